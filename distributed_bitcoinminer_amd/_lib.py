@@ -1,0 +1,184 @@
+"""ctypes binding of libhipminer.so (include/hipminer.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
+distributed_bitcoinminer_amd/csrc``).  There is no fallback: if the library or
+a GPU is missing, the calls raise ``HipMinerError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhipminer.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "hipminer.h")
+
+HM_OK = 0
+HM_ERR_INVALID = -1
+HM_ERR_NO_DEVICE = -2
+HM_ERR_HIP = -3
+HM_ERR_NOMEM = -4
+HM_ERR_RCCL = -5
+HM_ERR_INTERNAL = -6
+
+HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED = 0, 1, 2
+HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU = 1, 2, 3
+
+
+class HipMinerError(RuntimeError):
+    def __init__(self, rc: int, what: str = ""):
+        self.rc = rc
+        msg = strerror(rc) if _lib_or_none() else f"rc={rc}"
+        super().__init__(f"{what}: {msg} (rc={rc})" if what else f"{msg} (rc={rc})")
+
+
+class hm_result(ctypes.Structure):
+    _fields_ = [("hash", ctypes.c_uint64), ("nonce", ctypes.c_uint64)]
+
+
+class hm_stats(ctypes.Structure):
+    _fields_ = [("wall_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("dom_kernel_ms", ctypes.c_double), ("nonces", ctypes.c_uint64),
+                ("dom_nonces", ctypes.c_uint64), ("dom_compressions", ctypes.c_uint64),
+                ("launches", ctypes.c_int32), ("dom_kind", ctypes.c_int32),
+                ("ndev", ctypes.c_int32), ("dom_grid", ctypes.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _lib_or_none():
+    return _lib
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree libhipminer.so; raise if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise HipMinerError(HM_ERR_NO_DEVICE,
+                                f"{LIB_PATH} missing: run __graft_entry__.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.c_char_p
+        lib.hm_hash.restype = ctypes.c_uint64
+        lib.hm_hash.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64]
+        lib.hm_open.restype = ctypes.c_int
+        lib.hm_open.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_void_p)]
+        lib.hm_scan.restype = ctypes.c_int
+        lib.hm_scan.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.c_uint64,
+                                ctypes.c_uint64, ctypes.POINTER(hm_result)]
+        lib.hm_scan_stats.restype = ctypes.c_int
+        lib.hm_scan_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats)]
+        lib.hm_set_option.restype = ctypes.c_int
+        lib.hm_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]
+        lib.hm_strerror.restype = ctypes.c_char_p
+        lib.hm_strerror.argtypes = [ctypes.c_int]
+        lib.hm_close.restype = None
+        lib.hm_close.argtypes = [ctypes.c_void_p]
+        lib.hm_version.restype = ctypes.c_int
+        lib.hm_version.argtypes = []
+        lib.hm_debug_plan.restype = ctypes.c_int
+        lib.hm_debug_plan.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+        _lib = lib
+        return lib
+
+
+def strerror(rc: int) -> str:
+    return load().hm_strerror(rc).decode()
+
+
+def header_symbols() -> list[str]:
+    """Function names declared in include/hipminer.h."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(hm_[a-z_]+)\s*\(", text)))
+
+
+def as_bytes(msg) -> bytes:
+    """Go strings are byte strings; str is encoded as UTF-8 (Go source literals)."""
+    return msg.encode("utf-8") if isinstance(msg, str) else bytes(msg)
+
+
+class Context:
+    """One hipminer context (hm_open .. hm_close) on a set of HIP devices."""
+
+    def __init__(self, devices=None):
+        lib = load()
+        handle = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = lib.hm_open(arr, len(devices), ctypes.byref(handle))
+        else:
+            rc = lib.hm_open(None, 0, ctypes.byref(handle))
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_open")
+        self._h = handle
+        self._lib = lib
+
+    def scan(self, msg, lo: int, hi: int) -> tuple[int, int]:
+        m = as_bytes(msg)
+        out = hm_result()
+        rc = self._lib.hm_scan(self._h, m, len(m), lo, hi, ctypes.byref(out))
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_scan")
+        return int(out.hash), int(out.nonce)
+
+    def stats(self) -> dict:
+        st = hm_stats()
+        rc = self._lib.hm_scan_stats(self._h, ctypes.byref(st))
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_scan_stats")
+        return st.as_dict()
+
+    def set_option(self, opt: int, value: int) -> None:
+        rc = self._lib.hm_set_option(self._h, opt, value)
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_set_option")
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.hm_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_hash(msg, nonce: int) -> int:
+    """hm_hash: bitcoin.Hash on the host (hash.go:13-17)."""
+    m = as_bytes(msg)
+    return int(load().hm_hash(m, len(m), nonce))
+
+
+def debug_plan(msg, lo: int, hi: int, force_generic: bool = False) -> list[dict]:
+    m = as_bytes(msg)
+    cap = 32
+    buf = (ctypes.c_int64 * (8 * cap))()
+    n = load().hm_debug_plan(m, len(m), lo, hi, int(force_generic), buf, cap)
+    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle")
+    out = []
+    for i in range(min(n, cap)):
+        row = dict(zip(keys, buf[8 * i: 8 * i + 8]))
+        row["lo"] &= (1 << 64) - 1
+        row["hi"] &= (1 << 64) - 1
+        out.append(row)
+    return out

@@ -1,0 +1,508 @@
+// api.cpp -- the hipminer C ABI (include/hipminer.h).
+//
+// Replaces, inside the Go miner process, the scan of evalRoutine
+// (cmu440/bitcoin/miner/miner.go:63-76) and bitcoin.Hash
+// (cmu440/bitcoin/hash.go:13-17).  Per device and per call:
+//
+//   host:  plan_message (midstate) -> plan_range (digit segments, layouts)
+//   GPU :  per segment, on one of kStreams HIP streams
+//            [tiled]   hm_tile_plan_kernel -> counter reset -> hm_tiled_kernel
+//            [generic] hm_generic_kernel
+//          -> hm_fold_kernel (per-wave candidates -> per-stream best)
+//          -> join streams -> hm_fold_kernel (stream bests -> 16-B result)
+//   multi-device: contiguous shards, then either a host merge of the 16-B
+//          results or an RCCL all-gather of them (HM_OPT_MERGE_RCCL).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/hipminer.h"
+#include "kernels.hpp"
+#include "plan.hpp"
+
+using namespace hm;
+
+namespace {
+
+constexpr int kStreams = 4;
+
+struct Launch {
+    hipEvent_t start, stop;
+    uint64_t nonces;
+    int kind;
+    int grid;
+    uint32_t compressions;
+};
+
+struct Device {
+    int ordinal = -1;
+    int cus = 0;
+    hipStream_t stream[kStreams] = {};
+    uint32_t* rec[kStreams] = {};
+    uint64_t* cand[kStreams] = {};
+    unsigned int* counter[kStreams] = {};
+    uint64_t* best = nullptr;      // [kStreams][2]
+    uint64_t* result = nullptr;    // [2]
+    uint64_t* gathered = nullptr;  // [2 * ndev] (RCCL merge)
+    hm_result* host_out = nullptr; // pinned
+    hipEvent_t join[kStreams] = {};
+    std::vector<hipEvent_t> evpool;
+    size_t evnext = 0;
+    std::vector<Launch> launches;
+    ncclComm_t comm = nullptr;
+};
+
+bool debug_on() {
+    static const bool on = getenv("HM_DEBUG") != nullptr;
+    return on;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    if (debug_on()) fprintf(stderr, "hipminer: %s: %s\n", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? HM_ERR_NOMEM : HM_ERR_HIP;
+}
+
+#define HIPCHK(expr)                                   \
+    do {                                               \
+        hipError_t e_ = (expr);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+}  // namespace
+
+struct hm_ctx {
+    std::mutex mu;
+    std::vector<Device> devs;
+    bool force_generic = false;
+    bool merge_rccl = false;
+    int grid_per_cu = 0;
+    bool have_stats = false;
+    hm_stats last{};
+};
+
+namespace {
+
+int next_event(Device& dv, hipEvent_t* ev) {
+    if (dv.evnext == dv.evpool.size()) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        dv.evpool.push_back(e);
+    }
+    *ev = dv.evpool[dv.evnext++];
+    return HM_OK;
+}
+
+int device_init(Device& dv, int ordinal) {
+    dv.ordinal = ordinal;
+    HIPCHK(hipSetDevice(ordinal));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, ordinal));
+    dv.cus = prop.multiProcessorCount;
+    for (int s = 0; s < kStreams; ++s) {
+        HIPCHK(hipStreamCreateWithFlags(&dv.stream[s], hipStreamNonBlocking));
+        HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
+        HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
+        HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
+    }
+    HIPCHK(hipMalloc(&dv.best, kStreams * 2 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&dv.result, 2 * sizeof(uint64_t)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), sizeof(hm_result)));
+    return HM_OK;
+}
+
+void device_free(Device& dv) {
+    if (dv.ordinal < 0) return;
+    (void)hipSetDevice(dv.ordinal);
+    for (int s = 0; s < kStreams; ++s) {
+        if (dv.stream[s]) (void)hipStreamSynchronize(dv.stream[s]);
+    }
+    if (dv.comm) ncclCommDestroy(dv.comm);
+    for (int s = 0; s < kStreams; ++s) {
+        if (dv.rec[s]) (void)hipFree(dv.rec[s]);
+        if (dv.cand[s]) (void)hipFree(dv.cand[s]);
+        if (dv.counter[s]) (void)hipFree(dv.counter[s]);
+        if (dv.join[s]) (void)hipEventDestroy(dv.join[s]);
+        if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
+    }
+    for (hipEvent_t e : dv.evpool) (void)hipEventDestroy(e);
+    if (dv.best) (void)hipFree(dv.best);
+    if (dv.result) (void)hipFree(dv.result);
+    if (dv.gathered) (void)hipFree(dv.gathered);
+    if (dv.host_out) (void)hipHostFree(dv.host_out);
+    dv.ordinal = -1;
+}
+
+uint32_t count_compressions(const SegPlan& s) {
+    // SHA-256 compressions per nonce after the host midstate (SURVEY §8d "C").
+    return s.nb;
+}
+
+int tiled_grid(const hm_ctx* ctx, const Device& dv, const SegPlan& s, uint64_t ntasks) {
+    int per_cu = ctx->grid_per_cu;
+    if (per_cu <= 0) per_cu = tiled_blocks_per_cu(s.W1, s.straddle, s.trailer);
+    if (per_cu <= 0) per_cu = 1;
+    uint64_t grid = (uint64_t)per_cu * (uint64_t)dv.cus;
+    const uint64_t waves_per_block = kBlock / kWaveSize;
+    grid = std::min<uint64_t>(grid, (ntasks + waves_per_block - 1) / waves_per_block);
+    grid = std::min<uint64_t>(grid, kMaxCandWaves / waves_per_block);
+    return (int)std::max<uint64_t>(grid, 1);
+}
+
+// Enqueue one segment on stream `si`; records its launches for stats.
+int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si) {
+    hipStream_t st = dv.stream[si];
+    if (s.kind == HM_KIND_TILED) {
+        uint32_t kw[64] = {0};
+        if (s.trailer) trailer_kw(s, kw);
+        const uint64_t max_tiles =
+            std::min<uint64_t>(kMaxTilesPerLaunch, (uint64_t)0x7fffffffu / s.tpt);
+        for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
+            const uint64_t nt = std::min<uint64_t>(max_tiles, s.tile_hi - t + 1);
+            PlanArgs pa;
+            pa.rec = dv.rec[si];
+            pa.tile0 = t;
+            pa.pow10V = s.pow10V;
+            pa.total_bits = s.total_bits;
+            pa.ntiles = (uint32_t)nt;
+            pa.V = s.V;
+            pa.d = s.d;
+            pa.r = mp.r;
+            pa.fb = s.fb;
+            pa.nb = s.nb;
+            memcpy(pa.pw, mp.pw, sizeof pa.pw);
+            memcpy(pa.mid, mp.mid, sizeof pa.mid);
+            HIPCHK(launch_tile_plan(pa, st));
+            HIPCHK(hipMemsetAsync(dv.counter[si], 0, sizeof(unsigned int), st));
+            TiledArgs ta;
+            ta.rec = dv.rec[si];
+            ta.counter = dv.counter[si];
+            ta.cand = dv.cand[si];
+            ta.tile0 = t;
+            ta.pow10V = s.pow10V;
+            ta.seg_lo = s.lo;
+            ta.seg_hi = s.hi;
+            ta.ntasks = (uint32_t)(nt * s.tpt);
+            ta.tpt = s.tpt;
+            ta.vmax = (uint32_t)(pow10_u64(s.q) - 1);
+            ta.q = s.q;
+            ta.lane_shift = s.lane_shift;
+            ta.loop_shift = s.loop_shift;
+            memcpy(ta.trailer_kw, kw, sizeof kw);
+            const int grid = tiled_grid(ctx, dv, s, ta.ntasks);
+            Launch L;
+            int rc = next_event(dv, &L.start);
+            if (rc) return rc;
+            rc = next_event(dv, &L.stop);
+            if (rc) return rc;
+            // nonces of this launch: segment ∩ [t*10^V, (t+nt)*10^V - 1]
+            const uint64_t a = std::max(s.lo, t * s.pow10V);
+            const uint64_t b_tile_end = (t + nt) * s.pow10V - 1;  // may wrap past 2^64 - 1
+            const bool wraps = (t + nt) > (~0ull) / s.pow10V;
+            const uint64_t b = wraps ? s.hi : std::min(s.hi, b_tile_end);
+            L.nonces = b - a + 1;
+            L.kind = HM_KIND_TILED;
+            L.grid = grid;
+            L.compressions = count_compressions(s);
+            HIPCHK(hipEventRecord(L.start, st));
+            HIPCHK(launch_tiled(ta, s.W1, s.straddle, s.trailer, grid, st));
+            HIPCHK(hipEventRecord(L.stop, st));
+            HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize),
+                               dv.best + 2 * si, st));
+            dv.launches.push_back(L);
+            t += nt;
+            if (t == 0) break;  // tile index wrapped (cannot happen for d <= 20)
+        }
+        return HM_OK;
+    }
+    // generic
+    GenericArgs ga;
+    ga.cand = dv.cand[si];
+    ga.seg_lo = s.lo;
+    ga.count_m1 = s.hi - s.lo;
+    ga.total_bits = s.total_bits;
+    ga.d = s.d;
+    ga.r = mp.r;
+    ga.nb = s.nb;
+    memcpy(ga.pw, mp.pw, sizeof ga.pw);
+    memcpy(ga.mid, mp.mid, sizeof ga.mid);
+    const uint64_t need = ga.count_m1 / kBlock + 1;
+    const uint64_t cap = (uint64_t)(kMaxCandWaves / (kBlock / kWaveSize));
+    const int grid = (int)std::min<uint64_t>(need, std::min<uint64_t>(cap, (uint64_t)dv.cus * 8));
+    Launch L;
+    int rc = next_event(dv, &L.start);
+    if (rc) return rc;
+    rc = next_event(dv, &L.stop);
+    if (rc) return rc;
+    L.nonces = ga.count_m1 + 1;  // generic segments are far below 2^64
+    L.kind = HM_KIND_GENERIC;
+    L.grid = grid;
+    L.compressions = count_compressions(s);
+    HIPCHK(hipEventRecord(L.start, st));
+    HIPCHK(launch_generic(ga, grid, st));
+    HIPCHK(hipEventRecord(L.stop, st));
+    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), dv.best + 2 * si, st));
+    dv.launches.push_back(L);
+    return HM_OK;
+}
+
+// Enqueue the whole scan of [lo, hi] on one device; result lands in dv.result.
+int enqueue_device_scan(hm_ctx* ctx, Device& dv, const MsgPlan& mp, uint64_t lo, uint64_t hi,
+                        bool empty) {
+    HIPCHK(hipSetDevice(dv.ordinal));
+    dv.evnext = 0;
+    dv.launches.clear();
+    hipStream_t s0 = dv.stream[0];
+    HIPCHK(launch_init_best(dv.best, kStreams, s0));
+    HIPCHK(launch_init_best(dv.result, 1, s0));
+    if (empty) return HM_OK;
+    HIPCHK(hipEventRecord(dv.join[0], s0));
+    for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
+    std::vector<SegPlan> segs = plan_range(mp, lo, hi, ctx->force_generic);
+    // the largest segment on stream 0, the rest spread over streams 1..
+    size_t big = 0;
+    for (size_t i = 1; i < segs.size(); ++i)
+        if (segs[i].hi - segs[i].lo > segs[big].hi - segs[big].lo) big = i;
+    int rr = 0;
+    for (size_t i = 0; i < segs.size(); ++i) {
+        int si = 0;
+        if (i != big) si = 1 + (rr++ % (kStreams - 1));
+        int rc = enqueue_segment(ctx, dv, mp, segs[i], si);
+        if (rc) return rc;
+    }
+    for (int s = 1; s < kStreams; ++s) {
+        HIPCHK(hipEventRecord(dv.join[s], dv.stream[s]));
+        HIPCHK(hipStreamWaitEvent(s0, dv.join[s], 0));
+    }
+    HIPCHK(launch_fold(dv.best, kStreams, dv.result, s0));
+    return HM_OK;
+}
+
+bool lex_less(uint64_t k1, uint64_t n1, uint64_t k2, uint64_t n2) {
+    return k1 < k2 || (k1 == k2 && n1 < n2);
+}
+
+int rccl_merge(hm_ctx* ctx) {
+    const int n = (int)ctx->devs.size();
+    if (!ctx->devs[0].comm) {
+        std::vector<ncclComm_t> comms(n);
+        std::vector<int> ords(n);
+        for (int i = 0; i < n; ++i) ords[i] = ctx->devs[i].ordinal;
+        if (ncclCommInitAll(comms.data(), n, ords.data()) != ncclSuccess) return HM_ERR_RCCL;
+        for (int i = 0; i < n; ++i) {
+            ctx->devs[i].comm = comms[i];
+            HIPCHK(hipSetDevice(ctx->devs[i].ordinal));
+            HIPCHK(hipMalloc(&ctx->devs[i].gathered, (size_t)n * 2 * sizeof(uint64_t)));
+        }
+    }
+    if (ncclGroupStart() != ncclSuccess) return HM_ERR_RCCL;
+    for (int i = 0; i < n; ++i) {
+        Device& dv = ctx->devs[i];
+        HIPCHK(hipSetDevice(dv.ordinal));
+        if (ncclAllGather(dv.result, dv.gathered, 2, ncclUint64, dv.comm, dv.stream[0]) !=
+            ncclSuccess) {
+            ncclGroupEnd();
+            return HM_ERR_RCCL;
+        }
+    }
+    if (ncclGroupEnd() != ncclSuccess) return HM_ERR_RCCL;
+    // every rank now holds all candidates; rank 0 folds them
+    Device& d0 = ctx->devs[0];
+    HIPCHK(hipSetDevice(d0.ordinal));
+    HIPCHK(launch_init_best(d0.result, 1, d0.stream[0]));
+    HIPCHK(launch_fold(d0.gathered, (uint32_t)n, d0.result, d0.stream[0]));
+    return HM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
+    static const uint8_t empty = 0;
+    return host_hash(msg ? msg : &empty, msg ? len : 0, nonce);
+}
+
+int hm_version(void) { return (1 << 16) | 0; }
+
+const char* hm_strerror(int rc) {
+    switch (rc) {
+        case HM_OK: return "ok";
+        case HM_ERR_INVALID: return "invalid argument";
+        case HM_ERR_NO_DEVICE: return "no usable HIP device";
+        case HM_ERR_HIP: return "HIP runtime error (set HM_DEBUG=1 for details)";
+        case HM_ERR_NOMEM: return "out of memory";
+        case HM_ERR_RCCL: return "RCCL error";
+        case HM_ERR_INTERNAL: return "internal planner error";
+        default: return "unknown error";
+    }
+}
+
+int hm_open(const int* devices, int ndev, hm_ctx** out) {
+    if (!out || ndev < 0 || (ndev > 0 && !devices)) return HM_ERR_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return HM_ERR_NO_DEVICE;
+    std::vector<int> ords;
+    if (ndev == 0) {
+        for (int i = 0; i < count; ++i) ords.push_back(i);
+    } else {
+        for (int i = 0; i < ndev; ++i) {
+            if (devices[i] < 0 || devices[i] >= count) return HM_ERR_INVALID;
+            ords.push_back(devices[i]);
+        }
+    }
+    hm_ctx* ctx = new (std::nothrow) hm_ctx;
+    if (!ctx) return HM_ERR_NOMEM;
+    ctx->devs.resize(ords.size());
+    for (size_t i = 0; i < ords.size(); ++i) {
+        int rc = device_init(ctx->devs[i], ords[i]);
+        if (rc) {
+            for (auto& dv : ctx->devs) device_free(dv);
+            delete ctx;
+            return rc;
+        }
+    }
+    *out = ctx;
+    return HM_OK;
+}
+
+void hm_close(hm_ctx* ctx) {
+    if (!ctx) return;
+    {
+        std::lock_guard<std::mutex> g(ctx->mu);
+        for (auto& dv : ctx->devs) device_free(dv);
+    }
+    delete ctx;
+}
+
+int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
+    if (!ctx) return HM_ERR_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    switch (opt) {
+        case HM_OPT_FORCE_GENERIC: ctx->force_generic = value != 0; return HM_OK;
+        case HM_OPT_MERGE_RCCL: ctx->merge_rccl = value != 0; return HM_OK;
+        case HM_OPT_GRID_PER_CU:
+            if (value < 0 || value > 32) return HM_ERR_INVALID;
+            ctx->grid_per_cu = (int)value;
+            return HM_OK;
+        default: return HM_ERR_INVALID;
+    }
+}
+
+int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
+            hm_result* out) {
+    if (!ctx || !out || (!msg && len)) return HM_ERR_INVALID;
+    static const uint8_t empty_msg = 0;
+    if (!msg) msg = &empty_msg;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    const auto t0 = std::chrono::steady_clock::now();
+    const MsgPlan mp = plan_message(msg, len);
+    const int n = (int)ctx->devs.size();
+    const bool empty = lo > hi;
+    // contiguous shards: span_m1 + 1 = n*q + (rr + 1); shards 0..rr get q+1
+    const uint64_t span_m1 = empty ? 0 : hi - lo;
+    const uint64_t q = span_m1 / (uint64_t)n, rr = span_m1 % (uint64_t)n;
+    uint64_t start = lo;
+    std::vector<bool> dev_empty(n, empty);
+    for (int i = 0; i < n; ++i) {
+        uint64_t a = 0, b = 0;
+        bool e = empty;
+        if (!empty) {
+            const uint64_t cnt_m1 = q - 1u + ((uint64_t)i <= rr ? 1u : 0u);  // modular
+            e = (q == 0 && (uint64_t)i > rr);
+            a = start;
+            b = start + cnt_m1;
+            if (!e) start = b + 1;
+        }
+        dev_empty[i] = e;
+        int rc = enqueue_device_scan(ctx, ctx->devs[i], mp, a, b, e);
+        if (rc) return rc;
+    }
+    hm_result res{~0ull, 0};
+    if (n > 1 && ctx->merge_rccl) {
+        int rc = rccl_merge(ctx);
+        if (rc) return rc;
+        Device& d0 = ctx->devs[0];
+        HIPCHK(hipSetDevice(d0.ordinal));
+        HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, sizeof(hm_result), hipMemcpyDeviceToHost,
+                              d0.stream[0]));
+        for (auto& dv : ctx->devs) {
+            HIPCHK(hipSetDevice(dv.ordinal));
+            HIPCHK(hipStreamSynchronize(dv.stream[0]));
+        }
+        res = *d0.host_out;
+    } else {
+        for (auto& dv : ctx->devs) {
+            HIPCHK(hipSetDevice(dv.ordinal));
+            HIPCHK(hipMemcpyAsync(dv.host_out, dv.result, sizeof(hm_result),
+                                  hipMemcpyDeviceToHost, dv.stream[0]));
+        }
+        for (auto& dv : ctx->devs) {
+            HIPCHK(hipSetDevice(dv.ordinal));
+            HIPCHK(hipStreamSynchronize(dv.stream[0]));
+            if (lex_less(dv.host_out->hash, dv.host_out->nonce, res.hash, res.nonce))
+                res = *dv.host_out;
+        }
+    }
+    // stats
+    hm_stats st{};
+    st.ndev = n;
+    st.nonces = empty ? 0 : span_m1 + 1;  // wraps to 0 for the full 2^64 range
+    for (auto& dv : ctx->devs) {
+        for (auto& L : dv.launches) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, L.start, L.stop));
+            st.kernel_ms += ms;
+            st.launches += 1;
+            if (L.nonces > st.dom_nonces) {
+                st.dom_nonces = L.nonces;
+                st.dom_kernel_ms = ms;
+                st.dom_compressions = L.compressions;
+                st.dom_kind = L.kind;
+                st.dom_grid = L.grid;
+            }
+        }
+    }
+    st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+                     .count();
+    ctx->last = st;
+    ctx->have_stats = true;
+    *out = res;
+    return HM_OK;
+}
+
+int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
+    if (!ctx || !out || !ctx->have_stats) return HM_ERR_INVALID;
+    *out = ctx->last;
+    return HM_OK;
+}
+
+// ---- debug exports for host-side tests (not part of include/hipminer.h) ----
+// Writes up to `cap` segment descriptors as 8 x int64:
+//   d, lo, hi, kind, W1, V, trailer, straddle
+int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
+                  int64_t* outv, int cap) {
+    if (lo > hi) return 0;
+    static const uint8_t empty = 0;
+    const MsgPlan mp = plan_message(msg ? msg : &empty, msg ? len : 0);
+    std::vector<SegPlan> segs = plan_range(mp, lo, hi, force_generic != 0);
+    int i = 0;
+    for (; i < (int)segs.size() && i < cap; ++i) {
+        const SegPlan& s = segs[i];
+        int64_t* o = outv + 8 * i;
+        o[0] = s.d; o[1] = (int64_t)s.lo; o[2] = (int64_t)s.hi; o[3] = s.kind;
+        o[4] = s.W1; o[5] = s.V; o[6] = s.trailer; o[7] = s.straddle;
+    }
+    return (int)segs.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,357 @@
+// kernels.hip -- gfx950 kernels of the min-hash nonce scan.
+//
+// Replaces the miner's sequential loop (cmu440/bitcoin/miner/miner.go:63-76)
+// over bitcoin.Hash (cmu440/bitcoin/hash.go:13-17).  Integer-VALU bound: no
+// MFMA, no LDS on the hot path, ~zero HBM traffic.
+//
+//   hm_tile_plan_kernel  one thread per tile: ASCII high digits, padding,
+//                        length, and (two-block tails) the chaining state
+//                        after the tail block that holds no varying digit.
+//   hm_tiled_kernel      persistent waves; per task 64 lanes x 100 loop
+//                        steps; one SHA-256 compression per nonce from the
+//                        tile state (+ a constant trailer block when the
+//                        padding spills); wave-uniform running min in SGPRs,
+//                        refreshed by a 64-lane shuffle reduce only when some
+//                        lane's H0 <= the wave's best H0.
+//   hm_generic_kernel    one nonce per lane with a byte-level tail builder;
+//                        small or irregular segments and cross-checks.
+//   hm_fold_kernel       second reduce pass (candidates -> 16-B best).
+#include <hip/hip_runtime.h>
+
+#include "kernels.hpp"
+#include "sha256_defs.hpp"
+
+namespace hm {
+
+#define DEV __device__ __forceinline__
+
+DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_rotateright32(x, n); }
+DEV uint32_t bsig0(uint32_t x) { return rotr(x, 2) ^ rotr(x, 13) ^ rotr(x, 22); }
+DEV uint32_t bsig1(uint32_t x) { return rotr(x, 6) ^ rotr(x, 11) ^ rotr(x, 25); }
+DEV uint32_t ssig0(uint32_t x) { return rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3); }
+DEV uint32_t ssig1(uint32_t x) { return rotr(x, 17) ^ rotr(x, 19) ^ (x >> 10); }
+// Ch = bfi(e, f, g); Maj = bfi(a ^ b, c, b)
+DEV uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return ((f ^ g) & e) ^ g; }
+DEV uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return ((b ^ c) & (a ^ b)) ^ b; }
+
+DEV uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+DEV uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
+// 64 rounds from state s over message m (m is clobbered into the schedule
+// window).  On return s[0] = a64, s[1] = a63 (= b64); with FULL all of a..h.
+template <bool FULL>
+DEV void sha_rounds(uint32_t s[8], uint32_t m[16]) {
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        uint32_t w;
+        if (i < 16) {
+            w = m[i];
+        } else {
+            w = ssig1(m[(i - 2) & 15]) + m[(i - 7) & 15] + ssig0(m[(i - 15) & 15]) + m[i & 15];
+            m[i & 15] = w;
+        }
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + (kK[i] + w);
+        const uint32_t t2 = bsig0(a) + maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+    }
+    s[0] = a; s[1] = b;
+    if (FULL) { s[2] = c; s[3] = d; s[4] = e; s[5] = f; s[6] = g; s[7] = h; }
+}
+
+// 64 rounds over a constant block given as K[i]+W[i] (wave-uniform).
+DEV void sha_rounds_kw(uint32_t s[8], const uint32_t* __restrict__ kw) {
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw[i];
+        const uint32_t t2 = bsig0(a) + maj(a, b, c);
+        h = g; g = f; f = e; e = d + t1;
+        d = c; c = b; b = a; a = t1 + t2;
+    }
+    s[0] = a; s[1] = b;
+}
+
+// Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
+DEV void wave_min(uint64_t& k, uint64_t& n) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, off, kWaveSize);
+        const uint64_t n2 = __shfl_xor(n, off, kWaveSize);
+        const bool take = (k2 < k) || (k2 == k && n2 < n);
+        k = take ? k2 : k;
+        n = take ? n2 : n;
+    }
+}
+
+DEV void put_byte(uint32_t* w, uint32_t pos, uint32_t byte) {
+    w[pos >> 2] |= byte << (24u - 8u * (pos & 3u));
+}
+
+// ---------------------------------------------------------------------------
+// Tile planner
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) hm_tile_plan_kernel(const PlanArgs A) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.ntiles) return;
+    uint32_t w[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) w[k] = k < 16 ? A.pw[k] : 0u;
+    uint64_t x = (A.tile0 + i) * A.pow10V;  // tile base: low V digits are zero
+    for (int j = (int)A.d - 1; j >= 0; --j) {
+        const uint64_t y = x / 10u;
+        const uint32_t dig = (uint32_t)(x - y * 10u);
+        x = y;
+        if ((uint32_t)j < A.d - A.V) put_byte(w, A.r + (uint32_t)j, 0x30u + dig);
+    }
+    put_byte(w, A.r + A.d, 0x80u);
+    w[16 * A.nb - 2] = (uint32_t)(A.total_bits >> 32);
+    w[16 * A.nb - 1] = (uint32_t)A.total_bits;
+    uint32_t st[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) st[k] = A.mid[k];
+    uint32_t* out = A.rec + (size_t)i * kRecWords;
+    if (A.fb == 1) {
+        h_compress(st, w);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) out[8 + k] = w[16 + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) out[8 + k] = w[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) out[k] = st[k];
+}
+
+// ---------------------------------------------------------------------------
+// Tiled scan (the hot kernel)
+// ---------------------------------------------------------------------------
+template <int W1, bool STRADDLE, bool TRAILER>
+__global__ void __launch_bounds__(kBlock) hm_tiled_kernel(const TiledArgs A) {
+    static_assert(W1 >= 1 && W1 <= 15, "varying words are W[W1-1], W[W1]");
+    const uint32_t lane = __lane_id();
+    const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
+    uint32_t best_hi = 0xffffffffu, best_lo = 0xffffffffu;  // wave-uniform (SGPR)
+    uint64_t best_nonce = 0;
+
+    for (;;) {
+        uint32_t task = 0;
+        if (lane == 0) task = atomicAdd(A.counter, 1u);
+        task = uni(task);
+        if (task >= A.ntasks) break;
+        const uint32_t tile = task / A.tpt;
+        const uint32_t chunk = task - tile * A.tpt;
+        const uint32_t* __restrict__ R = A.rec + (size_t)tile * kRecWords;
+        uint32_t st[8], W[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) st[k] = R[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) W[k] = R[8 + k];
+
+        uint32_t v = chunk * kWaveSize + lane;
+        v = v > A.vmax ? A.vmax : v;  // surplus lanes repeat a valid nonce
+        uint64_t packed = 0;
+        uint32_t x = v;
+        for (uint32_t k = 0; k < A.q; ++k) {
+            const uint32_t y = x / 10u;
+            packed |= (uint64_t)(0x30u + x - y * 10u) << (8u * k);
+            x = y;
+        }
+        packed <<= A.lane_shift;
+        const uint32_t X0 = W[W1 - 1] | (uint32_t)(packed >> 32);
+        const uint32_t X1 = W[W1] | (uint32_t)packed;
+        const uint64_t nbase = (A.tile0 + tile) * A.pow10V + (uint64_t)v * 100u;
+
+        for (uint32_t t1 = 0; t1 < 10; ++t1) {
+            for (uint32_t t0 = 0; t0 < 10; ++t0) {
+                const uint64_t L = (uint64_t)(((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift;
+                uint32_t m[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) m[k] = W[k];
+                m[W1 - 1] = STRADDLE ? X0 + (uint32_t)(L >> 32) : X0;
+                m[W1] = X1 + (uint32_t)L;
+                uint32_t s[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s[k] = st[k];
+                uint32_t h0, h1;
+                if constexpr (TRAILER) {
+                    sha_rounds<true>(s, m);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) s[k] += st[k];
+                    const uint32_t o0 = s[0], o1 = s[1];
+                    sha_rounds_kw(s, A.trailer_kw);
+                    h0 = s[0] + o0;
+                    h1 = s[1] + o1;
+                } else {
+                    sha_rounds<false>(s, m);
+                    h0 = s[0] + st[0];
+                    h1 = s[1] + st[1];
+                }
+                const bool cand = h0 <= best_hi;
+                if (__builtin_amdgcn_ballot_w64(cand)) {
+                    // rare: some lane may beat the wave's best
+                    uint64_t key = ((uint64_t)h0 << 32) | h1;
+                    uint64_t n = nbase + t1 * 10u + t0;
+                    const bool ok = cand && n >= A.seg_lo && n <= A.seg_hi;
+                    if (!ok) { key = ~0ull; n = ~0ull; }
+                    wave_min(key, n);
+                    key = uni64(key);
+                    n = uni64(n);
+                    const uint64_t bk = ((uint64_t)best_hi << 32) | best_lo;
+                    if (key < bk || (key == bk && n < best_nonce)) {
+                        best_hi = (uint32_t)(key >> 32);
+                        best_lo = (uint32_t)key;
+                        best_nonce = n;
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        A.cand[2 * wslot] = ((uint64_t)best_hi << 32) | best_lo;
+        A.cand[2 * wslot + 1] = best_nonce;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic scan: one nonce per lane, any layout
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t bk = ~0ull, bn = 0;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.count_m1;) {
+        const uint64_t n = A.seg_lo + k;
+        uint32_t w[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) w[j] = j < 16 ? A.pw[j] : 0u;
+        uint64_t x = n;
+        for (int j = (int)A.d - 1; j >= 0; --j) {
+            const uint64_t y = x / 10u;
+            put_byte(w, A.r + (uint32_t)j, 0x30u + (uint32_t)(x - y * 10u));
+            x = y;
+        }
+        put_byte(w, A.r + A.d, 0x80u);
+        w[16 * A.nb - 2] = (uint32_t)(A.total_bits >> 32);
+        w[16 * A.nb - 1] = (uint32_t)A.total_bits;
+        uint32_t st[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st[j] = A.mid[j];
+        h_compress(st, w);
+        if (A.nb == 2) h_compress(st, w + 16);
+        const uint64_t key = ((uint64_t)st[0] << 32) | st[1];
+        if (key < bk || (key == bk && n < bn)) { bk = key; bn = n; }
+        if (A.count_m1 - k < stride) break;
+        k += stride;
+    }
+    wave_min(bk, bn);
+    if (__lane_id() == 0) {
+        const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + threadIdx.x / kWaveSize;
+        A.cand[2 * wslot] = bk;
+        A.cand[2 * wslot + 1] = bn;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Second reduce pass and init
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restrict__ cand,
+                                                         uint32_t n, uint64_t* best) {
+    __shared__ uint64_t sk[kBlock / kWaveSize], sn[kBlock / kWaveSize];
+    uint64_t k = ~0ull, nn = ~0ull;
+    if (threadIdx.x == 0) { k = best[0]; nn = best[1]; }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t k2 = cand[2 * i], n2 = cand[2 * i + 1];
+        if (k2 < k || (k2 == k && n2 < nn)) { k = k2; nn = n2; }
+    }
+    wave_min(k, nn);
+    if (__lane_id() == 0) { sk[threadIdx.x / kWaveSize] = k; sn[threadIdx.x / kWaveSize] = nn; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWaveSize; ++w)
+            if (sk[w] < k || (sk[w] == k && sn[w] < nn)) { k = sk[w]; nn = sn[w]; }
+        best[0] = k;
+        best[1] = nn;
+    }
+}
+
+__global__ void hm_init_best_kernel(uint64_t* best, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { best[2 * i] = ~0ull; best[2 * i + 1] = 0; }  // (MaxUint64, 0): miner.go:65-66
+}
+
+// ---------------------------------------------------------------------------
+// Launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s) {
+    const uint32_t grid = (a.ntiles + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(hm_tile_plan_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+using TiledFn = void (*)(const TiledArgs);
+
+#define HM_T(W, S, T) &hm_tiled_kernel<W, S, T>
+// [trailer][straddle][W1]; nullptr = layout that cannot occur
+static const TiledFn kTiled[2][2][16] = {
+    {{nullptr, HM_T(1, false, false), HM_T(2, false, false), HM_T(3, false, false),
+      HM_T(4, false, false), HM_T(5, false, false), HM_T(6, false, false), HM_T(7, false, false),
+      HM_T(8, false, false), HM_T(9, false, false), HM_T(10, false, false),
+      HM_T(11, false, false), HM_T(12, false, false), HM_T(13, false, false), nullptr, nullptr},
+     {nullptr, HM_T(1, true, false), HM_T(2, true, false), HM_T(3, true, false),
+      HM_T(4, true, false), HM_T(5, true, false), HM_T(6, true, false), HM_T(7, true, false),
+      HM_T(8, true, false), HM_T(9, true, false), HM_T(10, true, false), HM_T(11, true, false),
+      HM_T(12, true, false), HM_T(13, true, false), nullptr, nullptr}},
+    {{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+      nullptr, nullptr, nullptr, HM_T(13, false, true), HM_T(14, false, true),
+      HM_T(15, false, true)},
+     {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+      nullptr, nullptr, nullptr, HM_T(13, true, true), HM_T(14, true, true),
+      HM_T(15, true, true)}}};
+#undef HM_T
+
+static TiledFn tiled_fn(int W1, bool straddle, bool trailer) {
+    if (W1 < 1 || W1 > 15) return nullptr;
+    return kTiled[trailer ? 1 : 0][straddle ? 1 : 0][W1];
+}
+
+hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
+                        hipStream_t s) {
+    TiledFn fn = tiled_fn(W1, straddle, trailer);
+    if (!fn) return hipErrorInvalidValue;
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+int tiled_blocks_per_cu(int W1, bool straddle, bool trailer) {
+    TiledFn fn = tiled_fn(W1, straddle, trailer);
+    if (!fn) return 0;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(fn),
+                                                     kBlock, 0) != hipSuccess)
+        return 0;
+    return nb;
+}
+
+hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s) {
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(hm_generic_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s) {
+    hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, best);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s) {
+    hipLaunchKernelGGL(hm_init_best_kernel, dim3((n + 63) / 64), dim3(64), 0, s, best, n);
+    return hipGetLastError();
+}
+
+}  // namespace hm

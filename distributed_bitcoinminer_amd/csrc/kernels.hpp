@@ -1,0 +1,83 @@
+// kernels.hpp -- argument blocks and launchers of the gfx950 scan kernels.
+//
+// Hot path replaced: the miner scan loop (cmu440/bitcoin/miner/miner.go:63-76)
+// calling bitcoin.Hash (cmu440/bitcoin/hash.go:13-17) once per nonce.
+//
+// Work decomposition:
+//   segment  = nonces with the same decimal digit count d (message layout fixed)
+//   tile     = 10^V consecutive nonces sharing the high d-V digits; its
+//              record (chaining state + final-block words) is built once on
+//              the GPU by hm_tile_plan_kernel
+//   task     = one wave: 64 lanes x 100 loop steps; lane digits (q = V-2)
+//              vary per lane, the last two digits are the uniform loop index
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hm {
+
+constexpr int kWaveSize = 64;
+constexpr int kBlock = 256;            // 4 waves per workgroup
+constexpr int kRecWords = 32;          // tile record stride: state[8], W[16], pad
+constexpr uint32_t kMaxTilesPerLaunch = 1u << 20;
+constexpr uint32_t kMaxCandWaves = 32768;  // per-launch candidate slots (waves)
+
+// Tile planner: one thread per tile.
+struct PlanArgs {
+    uint32_t* rec;       // out: ntiles * kRecWords
+    uint64_t tile0;      // absolute tile index of record 0 (tile h = [h*10^V, (h+1)*10^V))
+    uint64_t pow10V;
+    uint64_t total_bits; // message bit length (len(msg) + 1 + d) * 8
+    uint32_t ntiles;
+    uint32_t V;          // varying low digits (left zero in the record)
+    uint32_t d;          // digit count of the segment
+    uint32_t r;          // prefix-remainder bytes in front of the digits
+    uint32_t fb;         // tail block holding the last digit (0/1)
+    uint32_t nb;         // tail blocks incl. a constant trailer (1/2)
+    uint32_t pw[16];     // prefix remainder, big-endian words, zero padded
+    uint32_t mid[8];     // midstate after the floor((len+1)/64) constant blocks
+};
+
+// Tiled scan: persistent waves pull tasks from a counter.
+struct TiledArgs {
+    const uint32_t* rec;
+    unsigned int* counter;
+    uint64_t* cand;      // 2 x u64 per wave slot: (key, nonce)
+    uint64_t tile0;
+    uint64_t pow10V;
+    uint64_t seg_lo, seg_hi;
+    uint32_t ntasks;
+    uint32_t tpt;        // tasks per tile = ceil(10^q / 64)
+    uint32_t vmax;       // 10^q - 1
+    uint32_t q;          // lane digits
+    uint32_t lane_shift; // bit offset of the lowest lane digit in the (W[W1-1]:W[W1]) pair
+    uint32_t loop_shift; // bit offset of the units loop digit (tens digit at +8)
+    uint32_t trailer_kw[64];  // K[i]+W[i] of the constant trailer block (TRAILER only)
+};
+
+// Generic scan: one nonce per lane (small / irregular segments, cross-checks).
+struct GenericArgs {
+    uint64_t* cand;
+    uint64_t seg_lo;
+    uint64_t count_m1;   // nonces - 1
+    uint64_t total_bits;
+    uint32_t d, r, nb;
+    uint32_t pw[16];
+    uint32_t mid[8];
+};
+
+// Launchers (return hipError_t of the launch).
+hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s);
+// W1 in [1, 15], straddle: loop tens digit in W[W1-1], trailer: constant
+// final block after the digit block.  Returns hipErrorInvalidValue for an
+// unsupported combination.
+hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
+                        hipStream_t s);
+hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s);
+// Fold n (key, nonce) pairs plus *best into *best (lexicographic min).
+hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s);
+hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);
+// Occupancy-derived persistent grid (workgroups) for the tiled kernel.
+int tiled_blocks_per_cu(int W1, bool straddle, bool trailer);
+
+}  // namespace hm

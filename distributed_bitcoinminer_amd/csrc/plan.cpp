@@ -1,0 +1,146 @@
+// plan.cpp -- host planner (see plan.hpp and DESIGN.md §3).
+#include "plan.hpp"
+
+#include <string.h>
+
+#include <algorithm>
+
+#include "../../include/hipminer.h"
+#include "sha256_defs.hpp"
+
+namespace hm {
+
+uint32_t digits_u64(uint64_t n) {
+    uint32_t d = 1;
+    while (n >= 10) { n /= 10; ++d; }
+    return d;
+}
+
+uint64_t pow10_u64(uint32_t k) {
+    uint64_t p = 1;
+    for (uint32_t i = 0; i < k; ++i) p *= 10u;
+    return p;
+}
+
+MsgPlan plan_message(const uint8_t* msg, uint64_t len) {
+    MsgPlan mp;
+    memcpy(mp.mid, kIV, sizeof mp.mid);
+    mp.len = len;
+    const uint64_t plen = len + 1;  // msg ‖ ' '
+    const uint64_t nconst = plen / 64;
+    uint8_t blk[64];
+    for (uint64_t b = 0; b < nconst; ++b) {
+        for (int i = 0; i < 64; ++i) {
+            const uint64_t p = 64 * b + i;
+            blk[i] = p < len ? msg[p] : 0x20;
+        }
+        uint32_t m[16];
+        h_load_block(m, blk);
+        h_compress(mp.mid, m);
+    }
+    mp.r = (uint32_t)(plen - 64 * nconst);
+    memset(blk, 0, sizeof blk);
+    for (uint32_t i = 0; i < mp.r; ++i) {
+        const uint64_t p = 64 * nconst + i;
+        blk[i] = p < len ? msg[p] : 0x20;
+    }
+    h_load_block(mp.pw, blk);
+    return mp;
+}
+
+static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
+    s.T = mp.r + s.d;
+    s.nb = (s.T + 9 <= 64) ? 1 : 2;
+    s.fb = (s.T - 1) / 64;
+    s.p_end = (s.T - 1) % 64;
+    s.total_bits = (mp.len + 1 + s.d) * 8;
+    s.kind = HM_KIND_GENERIC;
+    s.W1 = (int)(s.p_end / 4);
+    const uint32_t k = s.p_end % 4;
+    s.straddle = (k == 0);
+    s.trailer = (s.nb - 1 > s.fb);
+    s.V = s.q = s.lane_shift = s.loop_shift = s.tpt = 0;
+    s.pow10V = 1;
+    s.tile_lo = s.tile_hi = 0;
+    if (force_generic || s.W1 < 1) return;
+    const uint32_t ds = (s.fb == 0) ? mp.r : 0;  // first digit byte within block fb
+    const uint32_t vs = std::max<uint32_t>(4u * (uint32_t)(s.W1 - 1), ds);
+    if (vs > s.p_end) return;
+    s.V = s.p_end - vs + 1;
+    if (s.V < 5) return;  // q >= 3 lane digits keeps surplus lanes under 3 %
+    s.q = s.V - 2;
+    s.lane_shift = 8u * (5u - k);
+    s.loop_shift = 8u * (3u - k);
+    s.pow10V = pow10_u64(s.V);
+    const uint64_t lanes = pow10_u64(s.q);
+    s.tpt = (uint32_t)((lanes + 63) / 64);
+    s.tile_lo = s.lo / s.pow10V;
+    s.tile_hi = s.hi / s.pow10V;
+    s.kind = HM_KIND_TILED;
+}
+
+std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic) {
+    std::vector<SegPlan> out;
+    const uint32_t d0 = digits_u64(lo), d1 = digits_u64(hi);
+    for (uint32_t d = d0; d <= d1; ++d) {
+        SegPlan s;
+        s.d = d;
+        const uint64_t dlo = d == 1 ? 0 : pow10_u64(d - 1);
+        const uint64_t dhi = d == 20 ? ~0ull : pow10_u64(d) - 1;
+        s.lo = std::max(lo, dlo);
+        s.hi = std::min(hi, dhi);
+        if (s.lo > s.hi) continue;
+        layout(mp, s, force_generic);
+        out.push_back(s);
+    }
+    return out;
+}
+
+uint64_t host_hash(const uint8_t* msg, uint64_t len, uint64_t nonce) {
+    char dig[24];
+    int nd = 0;
+    do { dig[nd++] = (char)('0' + nonce % 10); nonce /= 10; } while (nonce);
+    const uint64_t total = len + 1 + (uint64_t)nd;
+    uint32_t st[8];
+    memcpy(st, kIV, sizeof st);
+    uint8_t blk[64];
+    uint64_t pos = 0;
+    auto byte_at = [&](uint64_t p) -> uint8_t {
+        if (p < len) return msg[p];
+        if (p == len) return 0x20;
+        return (uint8_t)dig[nd - 1 - (int)(p - len - 1)];
+    };
+    while (total - pos >= 64) {
+        for (int i = 0; i < 64; ++i) blk[i] = byte_at(pos + i);
+        uint32_t m[16];
+        h_load_block(m, blk);
+        h_compress(st, m);
+        pos += 64;
+    }
+    uint8_t tail[128];
+    memset(tail, 0, sizeof tail);
+    const uint32_t rem = (uint32_t)(total - pos);
+    for (uint32_t i = 0; i < rem; ++i) tail[i] = byte_at(pos + i);
+    tail[rem] = 0x80;
+    const uint32_t tl = rem + 9 <= 64 ? 64 : 128;
+    const uint64_t bits = total * 8;
+    for (int i = 0; i < 8; ++i) tail[tl - 1 - i] = (uint8_t)(bits >> (8 * i));
+    for (uint32_t b = 0; b < tl; b += 64) {
+        uint32_t m[16];
+        h_load_block(m, tail + b);
+        h_compress(st, m);
+    }
+    return ((uint64_t)st[0] << 32) | st[1];
+}
+
+void trailer_kw(const SegPlan& s, uint32_t kw[64]) {
+    uint32_t w[64];
+    memset(w, 0, sizeof w);
+    if (s.T == 64) w[0] = 0x80000000u;  // 0x80 opens the trailer block
+    w[14] = (uint32_t)(s.total_bits >> 32);
+    w[15] = (uint32_t)s.total_bits;
+    h_schedule(w);
+    for (int i = 0; i < 64; ++i) kw[i] = kK[i] + w[i];
+}
+
+}  // namespace hm

@@ -1,0 +1,52 @@
+// plan.hpp -- host planner: splits [lo, hi] into digit-count segments and
+// picks each segment's kernel layout.  Pure host code (no HIP calls), so the
+// CPU test suite can exercise it through hm_plan_* debug exports.
+//
+// Bytes hashed per nonce (cmu440/bitcoin/hash.go:15):
+//     msg ‖ 0x20 ‖ decimal(nonce)
+// The first floor((len+1)/64) 64-byte blocks are nonce-independent and are
+// folded into a host midstate.  The remaining "tail" holds r = (len+1) % 64
+// prefix bytes, the d digits, 0x80 and the bit length, in nb (1 or 2) blocks.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace hm {
+
+struct MsgPlan {
+    uint32_t mid[8];    // midstate after the constant prefix blocks
+    uint32_t pw[16];    // prefix remainder as big-endian words (zero padded)
+    uint32_t r;         // prefix remainder length (0..63)
+    uint64_t len;       // message length in bytes
+};
+
+struct SegPlan {
+    uint32_t d;                 // digits of every nonce in [lo, hi]
+    uint64_t lo, hi;            // inclusive
+    uint32_t T, nb, fb;         // tail bytes before 0x80; tail blocks; block of last digit
+    uint32_t p_end;             // in-block byte index of the last digit
+    int kind;                   // HM_KIND_TILED or HM_KIND_GENERIC
+    // tiled layout
+    int W1;                     // word holding the last digit (varying words W1-1, W1)
+    bool straddle, trailer;
+    uint32_t V, q;              // varying digits; lane digits (V = q + 2 loop digits)
+    uint32_t lane_shift, loop_shift;
+    uint64_t pow10V;
+    uint32_t tpt;               // tasks (waves) per tile
+    uint64_t tile_lo, tile_hi;  // inclusive tile range
+    uint64_t total_bits;
+};
+
+uint32_t digits_u64(uint64_t n);
+uint64_t pow10_u64(uint32_t k);  // k <= 19
+MsgPlan plan_message(const uint8_t* msg, uint64_t len);
+// Segment list for inclusive [lo, hi] (lo <= hi).
+std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic);
+// Host SHA-256 of msg ‖ ' ' ‖ decimal(nonce), first 8 bytes big-endian.
+uint64_t host_hash(const uint8_t* msg, uint64_t len, uint64_t nonce);
+// K[i] + W[i] of the constant trailer block of a trailer segment.
+void trailer_kw(const SegPlan& s, uint32_t kw[64]);
+
+}  // namespace hm

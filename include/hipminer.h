@@ -1,0 +1,122 @@
+/*
+ * hipminer.h -- C ABI of the MI355X (gfx950) miner backend.
+ *
+ * Drop-in boundary for ONE hot path of alexsun705/distributed_bitcoinMiner:
+ * the miner's min-hash scan.  Reference interfaces replaced (paths relative to
+ * the reference root, cmu440/ = p1/src/github.com/cmu440/):
+ *
+ *   hm_hash  replaces  bitcoin.Hash(msg string, nonce uint64) uint64
+ *                      cmu440/bitcoin/hash.go:13-17
+ *   hm_scan  replaces  the scan loop of evalRoutine,
+ *                      cmu440/bitcoin/miner/miner.go:63-76
+ *                      (result = maxUint; index = 0; for i := lower; i < upper;
+ *                       i++ { hash := bitcoin.Hash(data, i); if hash < result ...})
+ *                      fed by bitcoin.Message{Data, Lower, Upper}
+ *                      (cmu440/bitcoin/message.go:18-23) and producing the
+ *                      values of bitcoin.NewResult(hash, nonce) (:38-44).
+ *
+ * The cgo binding a maintainer adds to the Go miner is in INTEGRATION.md.
+ *
+ * Semantics (bit-exact with the reference):
+ *   - bytes hashed per nonce: msg[0..len) ‖ 0x20 ‖ decimal(nonce)   (hash.go:15)
+ *   - key: first 8 bytes of SHA-256, big-endian                      (hash.go:16)
+ *   - hm_scan: lexicographic min of (key, nonce) over the INCLUSIVE range
+ *     [lo, hi], seeded with (UINT64_MAX, 0).  This equals the reference's
+ *     ascending strict-< loop, ties to the lowest nonce.  lo > hi gives
+ *     (UINT64_MAX, 0).  hi may be UINT64_MAX: the reference miner's
+ *     `upper := Upper+1` wrap (miner.go:69) is NOT applied here; callers that
+ *     mirror evalRoutine apply it (see distributed_bitcoinminer_amd/miner.py).
+ *
+ * Ownership: msg is borrowed for the call only (never retained), so a cgo
+ * caller may pass Go memory.  `out` is written only when the call returns
+ * HM_OK.  The context owns its device buffers and streams.
+ *
+ * Threading: calls on one context are serialised by an internal mutex; every
+ * call re-binds its device (hipSetDevice), so Go may call from any OS thread.
+ *
+ * Errors: 0 = HM_OK; negative codes below; hm_strerror() describes them.
+ * Nothing aborts the process and there is no CPU fallback: a failed GPU scan
+ * is reported, never silently replaced.
+ */
+#ifndef HIPMINER_H
+#define HIPMINER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* 16 bytes: the (hash, nonce) candidate; also the RCCL all-gather element. */
+typedef struct hm_result {
+    uint64_t hash;
+    uint64_t nonce;
+} hm_result;
+
+typedef struct hm_ctx hm_ctx;
+
+/* Timing and work accounting of the most recent hm_scan on a context. */
+typedef struct hm_stats {
+    double wall_ms;          /* host wall time of the hm_scan call              */
+    double kernel_ms;        /* sum of scan-kernel durations (HIP events)        */
+    double dom_kernel_ms;    /* duration of the dominant (largest) scan launch   */
+    uint64_t nonces;         /* nonces covered by the call                       */
+    uint64_t dom_nonces;     /* nonces covered by the dominant launch            */
+    uint64_t dom_compressions; /* SHA-256 compressions per nonce after the host
+                                  midstate in the dominant launch (C of SURVEY
+                                  §8d; algorithmic, before any hoisting)         */
+    int32_t launches;        /* scan-kernel launches issued                      */
+    int32_t dom_kind;        /* HM_KIND_* of the dominant launch                 */
+    int32_t ndev;            /* devices used                                      */
+    int32_t dom_grid;        /* workgroups of the dominant launch                */
+} hm_stats;
+
+#define HM_OK 0
+#define HM_ERR_INVALID (-1)   /* bad argument                                   */
+#define HM_ERR_NO_DEVICE (-2) /* no usable HIP device / runtime                  */
+#define HM_ERR_HIP (-3)       /* a HIP runtime call failed                       */
+#define HM_ERR_NOMEM (-4)     /* device or host allocation failed                */
+#define HM_ERR_RCCL (-5)      /* an RCCL call failed                              */
+#define HM_ERR_INTERNAL (-6)  /* planner invariant violated                      */
+
+#define HM_KIND_NONE 0
+#define HM_KIND_GENERIC 1  /* one nonce per lane, generic tail builder          */
+#define HM_KIND_TILED 2    /* tile-planned final block (lane + loop digits)      */
+
+/* Options for hm_set_option. */
+#define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */
+#define HM_OPT_MERGE_RCCL 2    /* 1: merge multi-device candidates with RCCL     */
+#define HM_OPT_GRID_PER_CU 3   /* workgroups per CU for scan launches (0 = auto) */
+
+/* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
+ * to verify single results and for planning; needs no GPU. */
+uint64_t hm_hash(const uint8_t *msg, size_t len, uint64_t nonce);
+
+/* Open a context on `ndev` HIP devices (`devices` lists ordinals); ndev == 0
+ * uses every visible device.  Returns HM_ERR_NO_DEVICE without a GPU. */
+int hm_open(const int *devices, int ndev, hm_ctx **out);
+
+/* Min-hash scan of the inclusive range [lo, hi] (see semantics above).  With
+ * several devices the range is sharded contiguously and the per-device 16-B
+ * candidates are merged (RCCL all-gather when HM_OPT_MERGE_RCCL is set). */
+int hm_scan(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi,
+            hm_result *out);
+
+/* Stats of the last successful hm_scan on ctx. */
+int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
+
+int hm_set_option(hm_ctx *ctx, int opt, int64_t value);
+
+const char *hm_strerror(int rc);
+
+void hm_close(hm_ctx *ctx);
+
+/* ABI version: (major << 16) | minor. */
+int hm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIPMINER_H */

@@ -1,0 +1,115 @@
+"""CPU oracle for the reference's min-hash scan -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker or the timed CPU baseline.  The product
+path never routes through it.
+
+Two independent restatements of the reference hot path live here
+(paths relative to /root/reference, cmu440/ = p1/src/github.com/cmu440/):
+
+* ``py_hash`` / ``py_scan``: pure Python over ``hashlib`` (OpenSSL's SHA-256),
+  restating ``cmu440/bitcoin/hash.go:13-17`` and ``miner/miner.go:63-76``.
+  Slow (~1 MH/s); used for golden fixtures and small cases.
+* ``c_hash`` / ``c_scan`` / ``c_miner_eval``: ctypes over ``oracle/build/
+  liboracle.so`` (``oracle/hm_oracle.c``: its own FIPS 180-4 SHA-256 and the
+  Sprintf formatting), multi-threaded; used for larger parity ranges and as
+  the CPU baseline in bench.py.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import subprocess
+
+MAXU64 = (1 << 64) - 1
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    """Compile the C oracle in-tree (gcc; seconds)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        lib = ctypes.CDLL(_LIB_PATH)
+        lib.oracle_hash.restype = ctypes.c_uint64
+        lib.oracle_hash.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64]
+        for fn in (lib.oracle_scan, lib.oracle_miner_eval):
+            fn.restype = None
+            fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                           ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                           ctypes.POINTER(ctypes.c_uint64)]
+        lib.oracle_sha256.restype = None
+        lib.oracle_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+        _lib = lib
+    return _lib
+
+
+def _b(msg) -> bytes:
+    return msg.encode("utf-8") if isinstance(msg, str) else bytes(msg)
+
+
+# ---- pure-Python restatement (hashlib) -------------------------------------
+
+def py_hash(msg, nonce: int) -> int:
+    """hash.go:13-17: SHA256(Sprintf("%s %d", msg, nonce)), first 8 bytes BE."""
+    data = _b(msg) + b" " + str(int(nonce)).encode("ascii")
+    return int.from_bytes(hashlib.sha256(data).digest()[:8], "big")
+
+
+def py_scan(msg, lo: int, hi: int):
+    """miner.go:65-76 over inclusive [lo, hi]: strict <, ascending, init (MAX, 0)."""
+    result, index = MAXU64, 0
+    m = _b(msg)
+    for i in range(lo, hi + 1):
+        h = int.from_bytes(hashlib.sha256(m + b" " + str(i).encode()).digest()[:8], "big")
+        if h < result:
+            result, index = h, i
+    return result, index
+
+
+def py_miner_eval(msg, lower: int, upper: int):
+    """miner.go:67-76 with the `upper := Upper+1` uint64 wrap (:69)."""
+    up = (upper + 1) & MAXU64
+    if not lower < up:
+        return MAXU64, 0
+    return py_scan(msg, lower, up - 1)
+
+
+# ---- C restatement (ctypes) --------------------------------------------------
+
+def c_sha256(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    _load().oracle_sha256(data, len(data), out)
+    return out.raw
+
+
+def c_hash(msg, nonce: int) -> int:
+    m = _b(msg)
+    return int(_load().oracle_hash(m, len(m), nonce))
+
+
+def c_scan(msg, lo: int, hi: int, threads: int = 0):
+    m = _b(msg)
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    h, n = ctypes.c_uint64(), ctypes.c_uint64()
+    _load().oracle_scan(m, len(m), lo, hi, threads, ctypes.byref(h), ctypes.byref(n))
+    return int(h.value), int(n.value)
+
+
+def c_miner_eval(msg, lower: int, upper: int, threads: int = 0):
+    m = _b(msg)
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    h, n = ctypes.c_uint64(), ctypes.c_uint64()
+    _load().oracle_miner_eval(m, len(m), lower, upper, threads, ctypes.byref(h), ctypes.byref(n))
+    return int(h.value), int(n.value)

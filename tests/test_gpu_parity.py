@@ -1,0 +1,78 @@
+"""GPU parity: hm_scan through the C ABI vs golden fixtures and the CPU oracle.
+
+Bar: bit-exact (hash, nonce) -- this is integer/byte work.  Oracle-backed
+cases use sizes the C oracle finishes in seconds; full-size ranges are checked
+through size-independent properties (shard invariance, re-hash of the winner,
+kernel-vs-kernel agreement).
+"""
+import random
+
+import pytest
+
+from distributed_bitcoinminer_amd import _lib
+
+pytestmark = pytest.mark.gpu
+MAX = (1 << 64) - 1
+
+
+def test_golden_scans(ctx, golden):
+    for case in golden["scan_kats"]:
+        m = bytes.fromhex(case["msg_hex"])
+        lo, hi = int(case["lo"]), int(case["hi"])
+        got = ctx.scan(m, lo, hi)
+        assert got == (int(case["hash"]), int(case["nonce"])), (case["name"], lo, hi)
+
+
+def test_golden_scans_generic_kernel(ctx, golden):
+    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+    try:
+        for case in golden["scan_kats"][:60]:
+            m = bytes.fromhex(case["msg_hex"])
+            lo, hi = int(case["lo"]), int(case["hi"])
+            if hi - lo > 2_000_000:
+                continue
+            assert ctx.scan(m, lo, hi) == (int(case["hash"]), int(case["nonce"])), case["name"]
+    finally:
+        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+
+
+def test_config1_answer(ctx):
+    # client `bradfitz 10000000` -> the reference prints "Result 356393768206 7645578"
+    assert ctx.scan(b"bradfitz", 0, 10**7) == (356393768206, 7645578)
+    assert ctx.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+
+
+def test_single_nonce_kats(ctx, golden):
+    # lo == hi: the scan returns exactly (Hash(msg, n), n)
+    for case in golden["hash_kats"][::7]:
+        m = bytes.fromhex(case["msg_hex"])
+        n = int(case["nonce"])
+        assert ctx.scan(m, n, n) == (int(case["hash"]), n), (case["name"], n)
+
+
+def test_empty_range(ctx):
+    assert ctx.scan(b"bradfitz", 5, 4) == (MAX, 0)
+    assert ctx.scan(b"", MAX, 0) == (MAX, 0)
+
+
+def test_random_vs_oracle(ctx, oracle_mod):
+    """Random messages (0..130 B, every tail layout) x ranges across digit boundaries."""
+    rng = random.Random(2026)
+    for it in range(120):
+        L = rng.randrange(0, 131)
+        m = bytes(rng.randrange(256) for _ in range(L))
+        k = rng.randrange(1, 20)
+        c = 10 ** k
+        lo = max(0, c - rng.randrange(0, 40000))
+        hi = min(MAX, c + rng.randrange(0, 40000))
+        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
+
+
+def test_tiles_vs_oracle_medium(ctx, oracle_mod):
+    """Ranges spanning whole tiles (10^5..10^8 nonces per tile) for assorted layouts."""
+    rng = random.Random(7)
+    for L in (0, 3, 8, 20, 44, 45, 50, 54, 55, 56, 60, 63, 64, 70, 100, 119, 120, 127):
+        m = bytes(rng.randrange(32, 127) for _ in range(L))
+        lo = rng.randrange(10**9, 10**12)
+        hi = lo + 1_500_000
+        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
