@@ -18,6 +18,8 @@
 //   hm_fold_kernel       second reduce pass (candidates -> 16-B best).
 #include <hip/hip_runtime.h>
 
+#include <utility>
+
 #include "kernels.hpp"
 #include "sha256_defs.hpp"
 
@@ -26,11 +28,26 @@ namespace hm {
 #define DEV __device__ __forceinline__
 
 DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_rotateright32(x, n); }
-DEV uint32_t bsig0(uint32_t x) { return rotr(x, 2) ^ rotr(x, 13) ^ rotr(x, 22); }
-DEV uint32_t bsig1(uint32_t x) { return rotr(x, 6) ^ rotr(x, 11) ^ rotr(x, 25); }
-DEV uint32_t ssig0(uint32_t x) { return rotr(x, 7) ^ rotr(x, 18) ^ (x >> 3); }
-DEV uint32_t ssig1(uint32_t x) { return rotr(x, 17) ^ rotr(x, 19) ^ (x >> 10); }
-// Ch = bfi(e, f, g); Maj = bfi(a ^ b, c, b)
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one VALU op (LUT
+// index 4*src0 + 2*src1 + src2; 0x96 = three-way XOR).  hipcc forms bitop3
+// for Ch/Maj but not for XOR chains, so the Sigma functions use it directly.
+// Non-volatile asm: the compiler may still hoist/CSE it.
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// V = the value varies across lanes (VGPR): use bitop3; otherwise plain C so
+// the compiler folds wave-uniform work onto the scalar unit / hoists it.
+template <bool V> DEV uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    if constexpr (V) return xor3(a, b, c);
+    else return a ^ b ^ c;
+}
+template <bool V = true> DEV uint32_t bsig0(uint32_t x) { return x3<V>(rotr(x, 2), rotr(x, 13), rotr(x, 22)); }
+template <bool V = true> DEV uint32_t bsig1(uint32_t x) { return x3<V>(rotr(x, 6), rotr(x, 11), rotr(x, 25)); }
+template <bool V = true> DEV uint32_t ssig0(uint32_t x) { return x3<V>(rotr(x, 7), rotr(x, 18), x >> 3); }
+template <bool V = true> DEV uint32_t ssig1(uint32_t x) { return x3<V>(rotr(x, 17), rotr(x, 19), x >> 10); }
+// Ch = bfi(e, f, g); Maj = bfi(a ^ b, c, b) -- hipcc emits v_bitop3 for both
 DEV uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return ((f ^ g) & e) ^ g; }
 DEV uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return ((b ^ c) & (a ^ b)) ^ b; }
 
@@ -39,40 +56,76 @@ DEV uint64_t uni64(uint64_t x) {
     return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
 }
 
-// 64 rounds from state s over message m (m is clobbered into the schedule
-// window).  On return s[0] = a64, s[1] = a63 (= b64); with FULL all of a..h.
-template <bool FULL>
-DEV void sha_rounds(uint32_t s[8], uint32_t m[16]) {
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        uint32_t w;
-        if (i < 16) {
-            w = m[i];
-        } else {
-            w = ssig1(m[(i - 2) & 15]) + m[(i - 7) & 15] + ssig0(m[(i - 15) & 15]) + m[i & 15];
-            m[i & 15] = w;
-        }
-        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + (kK[i] + w);
-        const uint32_t t2 = bsig0(a) + maj(a, b, c);
-        h = g; g = f; f = e; e = d + t1;
-        d = c; c = b; b = a; a = t1 + t2;
+// Compile-time variability of the 64 schedule words given the mask VM of
+// message words that vary across lanes (bit i = W[i]).
+constexpr uint64_t sched_vary(uint32_t vm) {
+    uint64_t m = vm;
+    for (int t = 16; t < 64; ++t) {
+        const uint64_t dep = (m >> (t - 2)) | (m >> (t - 7)) | (m >> (t - 15)) | (m >> (t - 16));
+        if (dep & 1) m |= 1ull << t;
     }
-    s[0] = a; s[1] = b;
-    if (FULL) { s[2] = c; s[3] = d; s[4] = e; s[5] = f; s[6] = g; s[7] = h; }
+    return m;
+}
+constexpr int first_vary(uint32_t vm) {
+    int i = 0;
+    while (i < 16 && !((vm >> i) & 1)) ++i;
+    return i;
+}
+
+struct State { uint32_t a, b, c, d, e, f, g, h; };
+
+// One round I of a message block whose lane-varying words are VM.
+template <uint32_t VM, int I>
+DEV void round_step(State& s, uint32_t m[16]) {
+    constexpr uint64_t WV = sched_vary(VM);
+    constexpr int F = first_vary(VM);
+    uint32_t w;
+    if constexpr (I < 16) {
+        w = m[I];
+    } else {
+        constexpr bool v2 = (WV >> (I - 2)) & 1, v7 = (WV >> (I - 7)) & 1;
+        constexpr bool v15 = (WV >> (I - 15)) & 1, v16 = (WV >> (I - 16)) & 1;
+        // uniform terms summed first (scalar), lane-varying terms after
+        uint32_t u = 0, v = 0;
+        const uint32_t t2 = ssig1<v2>(m[(I - 2) & 15]);
+        const uint32_t t15 = ssig0<v15>(m[(I - 15) & 15]);
+        if constexpr (v2) v += t2; else u += t2;
+        if constexpr (v7) v += m[(I - 7) & 15]; else u += m[(I - 7) & 15];
+        if constexpr (v15) v += t15; else u += t15;
+        if constexpr (v16) v += m[I & 15]; else u += m[I & 15];
+        w = v + u;
+        m[I & 15] = w;
+    }
+    // a and e vary from the round after the first varying word enters
+    constexpr bool ev = I > F;
+    const uint32_t t1 = s.h + bsig1<ev>(s.e) + ch(s.e, s.f, s.g) + (kK[I] + w);
+    const uint32_t t2 = bsig0<ev>(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+template <uint32_t VM, int... I>
+DEV void rounds_seq(State& s, uint32_t m[16], std::integer_sequence<int, I...>) {
+    (round_step<VM, I>(s, m), ...);
+}
+
+// 64 rounds from state s over message m (m is clobbered into the schedule
+// window).  VM marks the words that vary across lanes.  On return s.a = a64,
+// s.b = a63 (= b64), the rest as well.
+template <uint32_t VM>
+DEV void sha_rounds(State& s, uint32_t m[16]) {
+    rounds_seq<VM>(s, m, std::make_integer_sequence<int, 64>{});
 }
 
 // 64 rounds over a constant block given as K[i]+W[i] (wave-uniform).
-DEV void sha_rounds_kw(uint32_t s[8], const uint32_t* __restrict__ kw) {
-    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+DEV void sha_rounds_kw(State& s, const uint32_t* __restrict__ kw) {
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
-        const uint32_t t1 = h + bsig1(e) + ch(e, f, g) + kw[i];
-        const uint32_t t2 = bsig0(a) + maj(a, b, c);
-        h = g; g = f; f = e; e = d + t1;
-        d = c; c = b; b = a; a = t1 + t2;
+        const uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + kw[i];
+        const uint32_t t2 = bsig0(s.a) + maj(s.a, s.b, s.c);
+        s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+        s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
     }
-    s[0] = a; s[1] = b;
 }
 
 // Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
@@ -129,8 +182,17 @@ __global__ void __launch_bounds__(kBlock) hm_tile_plan_kernel(const PlanArgs A) 
 // ---------------------------------------------------------------------------
 // Tiled scan (the hot kernel)
 // ---------------------------------------------------------------------------
+#ifndef HM_TILED_WAVES_PER_EU
+#define HM_TILED_WAVES_PER_EU 0
+#endif
+#if HM_TILED_WAVES_PER_EU > 0
+#define HM_TILED_BOUNDS __launch_bounds__(kBlock, HM_TILED_WAVES_PER_EU)
+#else
+#define HM_TILED_BOUNDS __launch_bounds__(kBlock)
+#endif
+
 template <int W1, bool STRADDLE, bool TRAILER>
-__global__ void __launch_bounds__(kBlock) hm_tiled_kernel(const TiledArgs A) {
+__global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
     static_assert(W1 >= 1 && W1 <= 15, "varying words are W[W1-1], W[W1]");
     const uint32_t lane = __lane_id();
     const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
@@ -173,22 +235,20 @@ __global__ void __launch_bounds__(kBlock) hm_tiled_kernel(const TiledArgs A) {
                 for (int k = 0; k < 16; ++k) m[k] = W[k];
                 m[W1 - 1] = STRADDLE ? X0 + (uint32_t)(L >> 32) : X0;
                 m[W1] = X1 + (uint32_t)L;
-                uint32_t s[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) s[k] = st[k];
+                constexpr uint32_t VM = (1u << (W1 - 1)) | (1u << W1);
+                State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+                sha_rounds<VM>(s, m);
                 uint32_t h0, h1;
                 if constexpr (TRAILER) {
-                    sha_rounds<true>(s, m);
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) s[k] += st[k];
-                    const uint32_t o0 = s[0], o1 = s[1];
-                    sha_rounds_kw(s, A.trailer_kw);
-                    h0 = s[0] + o0;
-                    h1 = s[1] + o1;
+                    State o{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
+                            s.e + st[4], s.f + st[5], s.g + st[6], s.h + st[7]};
+                    State t = o;
+                    sha_rounds_kw(t, A.trailer_kw);
+                    h0 = t.a + o.a;
+                    h1 = t.b + o.b;
                 } else {
-                    sha_rounds<false>(s, m);
-                    h0 = s[0] + st[0];
-                    h1 = s[1] + st[1];
+                    h0 = s.a + st[0];
+                    h1 = s.b + st[1];
                 }
                 const bool cand = h0 <= best_hi;
                 if (__builtin_amdgcn_ballot_w64(cand)) {
