@@ -23,7 +23,7 @@ HM_ERR_NOMEM = -4
 HM_ERR_RCCL = -5
 HM_ERR_INTERNAL = -6
 
-HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED = 0, 1, 2
+HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU = 1, 2, 3
 
 

@@ -47,6 +47,7 @@ struct Device {
     int cus = 0;
     hipStream_t stream[kStreams] = {};
     uint32_t* rec[kStreams] = {};
+    uint32_t* kwt[kStreams] = {};
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* best = nullptr;      // [kStreams][2]
@@ -110,6 +111,7 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipStreamCreateWithFlags(&dv.stream[s], hipStreamNonBlocking));
         HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
+        HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
     }
@@ -129,6 +131,7 @@ void device_free(Device& dv) {
     for (int s = 0; s < kStreams; ++s) {
         if (dv.rec[s]) (void)hipFree(dv.rec[s]);
         if (dv.cand[s]) (void)hipFree(dv.cand[s]);
+        if (dv.kwt[s]) (void)hipFree(dv.kwt[s]);
         if (dv.counter[s]) (void)hipFree(dv.counter[s]);
         if (dv.join[s]) (void)hipEventDestroy(dv.join[s]);
         if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
@@ -146,9 +149,8 @@ uint32_t count_compressions(const SegPlan& s) {
     return s.nb;
 }
 
-int tiled_grid(const hm_ctx* ctx, const Device& dv, const SegPlan& s, uint64_t ntasks) {
-    int per_cu = ctx->grid_per_cu;
-    if (per_cu <= 0) per_cu = tiled_blocks_per_cu(s.W1, s.straddle, s.trailer);
+int persistent_grid(const hm_ctx* ctx, const Device& dv, int per_cu_auto, uint64_t ntasks) {
+    int per_cu = ctx->grid_per_cu > 0 ? ctx->grid_per_cu : per_cu_auto;
     if (per_cu <= 0) per_cu = 1;
     uint64_t grid = (uint64_t)per_cu * (uint64_t)dv.cus;
     const uint64_t waves_per_block = kBlock / kWaveSize;
@@ -157,9 +159,78 @@ int tiled_grid(const hm_ctx* ctx, const Device& dv, const SegPlan& s, uint64_t n
     return (int)std::max<uint64_t>(grid, 1);
 }
 
+// nonces of [t*P, (t+nt)*P - 1] ∩ [lo, hi] (P = nonces per tile)
+uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
+    const uint64_t a = std::max(s.lo, t * s.pow10V);
+    const bool wraps = (t + nt) > (~0ull) / s.pow10V;
+    const uint64_t b = wraps ? s.hi : std::min(s.hi, (t + nt) * s.pow10V - 1);
+    return b - a + 1;
+}
+
+int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si) {
+    hipStream_t st = dv.stream[si];
+    HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.total_bits, st));
+    const uint64_t per_tile = (uint64_t)s.tpt * s.ntc;
+    const uint64_t max_tiles = std::min<uint64_t>(kMaxTilesPerLaunch, 0x7fffffffull / per_tile);
+    for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
+        const uint64_t nt = std::min<uint64_t>(max_tiles, s.tile_hi - t + 1);
+        PlanArgs pa;
+        pa.rec = dv.rec[si];
+        pa.tile0 = t;
+        pa.pow10V = s.pow10V;
+        pa.total_bits = s.total_bits;
+        pa.ntiles = (uint32_t)nt;
+        pa.V = s.V;
+        pa.d = s.d;
+        pa.r = mp.r;
+        pa.fb = 0;  // keep tail block 0 raw; its compression is per lane
+        pa.nb = s.nb;
+        memcpy(pa.pw, mp.pw, sizeof pa.pw);
+        memcpy(pa.mid, mp.mid, sizeof pa.mid);
+        HIPCHK(launch_tile_plan(pa, st));
+        HIPCHK(hipMemsetAsync(dv.counter[si], 0, sizeof(unsigned int), st));
+        ChainedArgs ca;
+        ca.rec = dv.rec[si];
+        ca.kwt = dv.kwt[si];
+        ca.counter = dv.counter[si];
+        ca.cand = dv.cand[si];
+        ca.tile0 = t;
+        ca.pow10qf = s.pow10V;
+        ca.pow10f = pow10_u64(s.f);
+        ca.seg_lo = s.lo;
+        ca.seg_hi = s.hi;
+        ca.ntasks = (uint32_t)(nt * per_tile);
+        ca.tpt = s.tpt;
+        ca.ntc = s.ntc;
+        ca.tch = s.tch;
+        ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
+        ca.q = s.q;
+        const int grid = persistent_grid(ctx, dv, chained_blocks_per_cu(), ca.ntasks);
+        Launch L;
+        int rc = next_event(dv, &L.start);
+        if (rc) return rc;
+        rc = next_event(dv, &L.stop);
+        if (rc) return rc;
+        L.nonces = tile_span_nonces(s, t, nt);
+        L.kind = HM_KIND_CHAINED;
+        L.grid = grid;
+        L.compressions = count_compressions(s);
+        HIPCHK(hipEventRecord(L.start, st));
+        HIPCHK(launch_chained(ca, grid, st));
+        HIPCHK(hipEventRecord(L.stop, st));
+        HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), dv.best + 2 * si,
+                           st));
+        dv.launches.push_back(L);
+        t += nt;
+        if (t == 0) break;
+    }
+    return HM_OK;
+}
+
 // Enqueue one segment on stream `si`; records its launches for stats.
 int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si) {
     hipStream_t st = dv.stream[si];
+    if (s.kind == HM_KIND_CHAINED) return enqueue_chained(ctx, dv, mp, s, si);
     if (s.kind == HM_KIND_TILED) {
         uint32_t kw[64] = {0};
         if (s.trailer) trailer_kw(s, kw);
@@ -197,18 +268,14 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.lane_shift = s.lane_shift;
             ta.loop_shift = s.loop_shift;
             memcpy(ta.trailer_kw, kw, sizeof kw);
-            const int grid = tiled_grid(ctx, dv, s, ta.ntasks);
+            const int grid = persistent_grid(
+                ctx, dv, tiled_blocks_per_cu(s.W1, s.straddle, s.trailer), ta.ntasks);
             Launch L;
             int rc = next_event(dv, &L.start);
             if (rc) return rc;
             rc = next_event(dv, &L.stop);
             if (rc) return rc;
-            // nonces of this launch: segment ∩ [t*10^V, (t+nt)*10^V - 1]
-            const uint64_t a = std::max(s.lo, t * s.pow10V);
-            const uint64_t b_tile_end = (t + nt) * s.pow10V - 1;  // may wrap past 2^64 - 1
-            const bool wraps = (t + nt) > (~0ull) / s.pow10V;
-            const uint64_t b = wraps ? s.hi : std::min(s.hi, b_tile_end);
-            L.nonces = b - a + 1;
+            L.nonces = tile_span_nonces(s, t, nt);
             L.kind = HM_KIND_TILED;
             L.grid = grid;
             L.compressions = count_compressions(s);

@@ -277,6 +277,106 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// Chained scan: per lane one compression of tail block 0 per task, then one
+// table-driven compression per loop value (the final block is wave-uniform).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) hm_kw_table_kernel(uint32_t* __restrict__ out,
+                                                             uint32_t f, uint32_t n,
+                                                             uint64_t total_bits) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    uint32_t w[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) w[k] = 0;
+    uint32_t x = t;
+    for (int j = (int)f - 1; j >= 0; --j) {  // f digits with leading zeros
+        const uint32_t y = x / 10u;
+        put_byte(w, (uint32_t)j, 0x30u + x - y * 10u);
+        x = y;
+    }
+    put_byte(w, f, 0x80u);
+    w[14] = (uint32_t)(total_bits >> 32);
+    w[15] = (uint32_t)total_bits;
+    h_schedule(w);
+    uint32_t* o = out + (size_t)t * 64;
+#pragma unroll
+    for (int k = 0; k < 64; ++k) o[k] = kK[k] + w[k];
+}
+
+__global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A) {
+    const uint32_t lane = __lane_id();
+    const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
+    uint32_t best_hi = 0xffffffffu, best_lo = 0xffffffffu;
+    uint64_t best_nonce = 0;
+    const uint32_t per_tile = A.tpt * A.ntc;
+
+    for (;;) {
+        uint32_t task = 0;
+        if (lane == 0) task = atomicAdd(A.counter, 1u);
+        task = uni(task);
+        if (task >= A.ntasks) break;
+        const uint32_t tile = task / per_tile;
+        const uint32_t rem = task - tile * per_tile;
+        const uint32_t chunk = rem / A.ntc;
+        const uint32_t tc = rem - chunk * A.ntc;
+        const uint32_t* __restrict__ R = A.rec + (size_t)tile * kRecWords;
+        uint32_t st[8], W[16];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) st[k] = R[k];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) W[k] = R[8 + k];
+
+        uint32_t v = chunk * kWaveSize + lane;
+        v = v > A.vmax ? A.vmax : v;
+        uint32_t packed = 0, x = v;
+        for (uint32_t k = 0; k < A.q; ++k) {
+            const uint32_t y = x / 10u;
+            packed |= (0x30u + x - y * 10u) << (8u * k);
+            x = y;
+        }
+        uint32_t m[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) m[k] = W[k];
+        m[15] = W[15] | packed;
+        State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+        sha_rounds<1u << 15>(s, m);
+        // chaining value into the final block (per lane)
+        const State cs{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
+                       s.e + st[4], s.f + st[5], s.g + st[6], s.h + st[7]};
+        const uint64_t nbase = (A.tile0 + tile) * A.pow10qf + (uint64_t)v * A.pow10f;
+        const uint32_t t_begin = tc * A.tch;
+        uint32_t t_end = t_begin + A.tch;
+        if (t_end > (uint32_t)A.pow10f) t_end = (uint32_t)A.pow10f;
+        const uint32_t* __restrict__ kw = A.kwt + (size_t)t_begin * 64;
+        for (uint32_t t = t_begin; t < t_end; ++t, kw += 64) {
+            State u = cs;
+            sha_rounds_kw(u, kw);
+            const uint32_t h0 = u.a + cs.a;
+            const bool cand = h0 <= best_hi;
+            if (__builtin_amdgcn_ballot_w64(cand)) {
+                uint64_t key = ((uint64_t)h0 << 32) | (u.b + cs.b);
+                uint64_t n = nbase + t;
+                const bool ok = cand && n >= A.seg_lo && n <= A.seg_hi;
+                if (!ok) { key = ~0ull; n = ~0ull; }
+                wave_min(key, n);
+                key = uni64(key);
+                n = uni64(n);
+                const uint64_t bk = ((uint64_t)best_hi << 32) | best_lo;
+                if (key < bk || (key == bk && n < best_nonce)) {
+                    best_hi = (uint32_t)(key >> 32);
+                    best_lo = (uint32_t)key;
+                    best_nonce = n;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        A.cand[2 * wslot] = ((uint64_t)best_hi << 32) | best_lo;
+        A.cand[2 * wslot + 1] = best_nonce;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic scan: one nonce per lane, any layout
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A) {
@@ -401,6 +501,30 @@ hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s) {
     if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(hm_generic_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s) {
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(hm_chained_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+int chained_blocks_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &nb, reinterpret_cast<const void*>(&hm_chained_kernel), kBlock, 0) != hipSuccess)
+        return 0;
+    return nb;
+}
+
+hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s) {
+    if (f < 1 || f > kMaxChainedF) return hipErrorInvalidValue;
+    uint32_t n = 1;
+    for (uint32_t i = 0; i < f; ++i) n *= 10u;
+    hipLaunchKernelGGL(hm_kw_table_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                       out, f, n, total_bits);
     return hipGetLastError();
 }
 

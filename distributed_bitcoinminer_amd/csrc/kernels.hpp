@@ -55,6 +55,29 @@ struct TiledArgs {
     uint32_t trailer_kw[64];  // K[i]+W[i] of the constant trailer block (TRAILER only)
 };
 
+// Chained scan (two-block tails whose final block holds only 1..4 digits):
+// lanes vary the last q digits of tail block 0 (word W15), the final
+// block's digits are the loop index t and its schedule comes from a table of
+// K[i]+W[i] (kMaxChainedTable entries x 64 words).
+constexpr uint32_t kMaxChainedF = 4;
+constexpr uint32_t kMaxChainedTable = 10000;
+struct ChainedArgs {
+    const uint32_t* rec;     // tile records (state = midstate, W = tail block 0)
+    const uint32_t* kwt;     // [10^f][64] K+W of the final block per loop value
+    unsigned int* counter;
+    uint64_t* cand;
+    uint64_t tile0;
+    uint64_t pow10qf;        // nonces per tile = 10^(q+f)
+    uint64_t pow10f;         // loop values = 10^f
+    uint64_t seg_lo, seg_hi;
+    uint32_t ntasks;
+    uint32_t tpt;            // lane chunks per tile = ceil(10^q / 64)
+    uint32_t ntc;            // loop chunks per lane chunk
+    uint32_t tch;            // loop values per loop chunk
+    uint32_t vmax;           // 10^q - 1
+    uint32_t q;              // lane digits (<= 4, all in W15)
+};
+
 // Generic scan: one nonce per lane (small / irregular segments, cross-checks).
 struct GenericArgs {
     uint64_t* cand;
@@ -74,6 +97,10 @@ hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s);
 hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
                         hipStream_t s);
 hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s);
+hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s);
+int chained_blocks_per_cu();
+// K+W table of the final block for loop values t in [0, 10^f).
+hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s);
 // Fold n (key, nonce) pairs plus *best into *best (lexicographic min).
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s);
 hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);

@@ -60,9 +60,32 @@ static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
     s.straddle = (k == 0);
     s.trailer = (s.nb - 1 > s.fb);
     s.V = s.q = s.lane_shift = s.loop_shift = s.tpt = 0;
+    s.f = s.tch = s.ntc = 0;
     s.pow10V = 1;
     s.tile_lo = s.tile_hi = 0;
-    if (force_generic || s.W1 < 1) return;
+    if (force_generic) return;
+    if (s.fb == 1 && s.T - 64 <= 4) {
+        // Chained: the final block holds only f <= 4 digits (uniform loop
+        // index, schedule from a K+W table); lanes vary the last q <= 4
+        // digits of tail block 0, i.e. word W15 only.
+        const uint32_t f = s.T - 64;
+        const uint32_t q = std::min<uint32_t>(4u, 64u - mp.r);
+        if (q >= 2) {
+            s.kind = HM_KIND_CHAINED;
+            s.f = f;
+            s.q = q;
+            s.V = q + f;
+            s.pow10V = pow10_u64(s.V);
+            s.tpt = (uint32_t)((pow10_u64(q) + 63) / 64);
+            const uint32_t nloop = (uint32_t)pow10_u64(f);
+            s.tch = std::min<uint32_t>(nloop, 1000u);
+            s.ntc = (nloop + s.tch - 1) / s.tch;
+            s.tile_lo = s.lo / s.pow10V;
+            s.tile_hi = s.hi / s.pow10V;
+            return;
+        }
+    }
+    if (s.W1 < 1) return;
     const uint32_t ds = (s.fb == 0) ? mp.r : 0;  // first digit byte within block fb
     const uint32_t vs = std::max<uint32_t>(4u * (uint32_t)(s.W1 - 1), ds);
     if (vs > s.p_end) return;

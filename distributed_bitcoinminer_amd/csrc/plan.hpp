@@ -34,7 +34,9 @@ struct SegPlan {
     uint32_t V, q;              // varying digits; lane digits (V = q + 2 loop digits)
     uint32_t lane_shift, loop_shift;
     uint64_t pow10V;
-    uint32_t tpt;               // tasks (waves) per tile
+    uint32_t tpt;               // lane chunks (waves) per tile
+    // chained layout (kind HM_KIND_CHAINED): f digits in the final block
+    uint32_t f, tch, ntc;       // final-block digits; loop values per task; loop chunks
     uint64_t tile_lo, tile_hi;  // inclusive tile range
     uint64_t total_bits;
 };

@@ -83,6 +83,7 @@ typedef struct hm_stats {
 #define HM_KIND_NONE 0
 #define HM_KIND_GENERIC 1  /* one nonce per lane, generic tail builder          */
 #define HM_KIND_TILED 2    /* tile-planned final block (lane + loop digits)      */
+#define HM_KIND_CHAINED 3  /* two-block tail: per-lane block 0, table-driven final block */
 
 /* Options for hm_set_option. */
 #define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */

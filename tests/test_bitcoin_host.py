@@ -108,6 +108,11 @@ def test_planner_layouts(L):
             assert first >= digit_start and first >= 4 * (s["W1"] - 1)
             assert s["W1"] >= 1
             assert (not s["trailer"]) or s["W1"] >= 13
+        elif s["kind"] == _lib.HM_KIND_CHAINED:
+            f = T - 64                              # digits in the final block
+            assert fb == 1 and 1 <= f <= 4
+            q = s["V"] - f                          # lane digits, all in W15 of block 0
+            assert 2 <= q <= 4 and q <= 64 - r
         else:
             assert s["kind"] == _lib.HM_KIND_GENERIC
     assert prev_hi == MAX

@@ -76,3 +76,60 @@ def test_tiles_vs_oracle_medium(ctx, oracle_mod):
         lo = rng.randrange(10**9, 10**12)
         hi = lo + 1_500_000
         assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
+
+
+def test_chained_layouts_vs_oracle(ctx, oracle_mod):
+    """Two-block tails whose final block holds 1..4 digits (chained kernel)."""
+    rng = random.Random(99)
+    seen = set()
+    for L in range(56, 130):
+        m = bytes(rng.randrange(33, 127) for _ in range(L))
+        r = (L + 1) % 64
+        for d in range(8, 21):
+            T = r + d
+            if T < 65 or T - 64 > 4:
+                continue
+            seg = [s for s in _lib.debug_plan(m, 10**(d - 1), 10**d - 1)][0]
+            if seg["kind"] != _lib.HM_KIND_CHAINED:
+                continue
+            seen.add((T - 64, seg["V"] - (T - 64)))
+            base = rng.randrange(10**(d - 1), 10**d - 300_000)
+            lo, hi = base, base + rng.randrange(1, 250_000)
+            assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
+    assert {(1, 4), (2, 4), (3, 4), (4, 4)} <= seen
+
+
+def test_long120_config3_slice(ctx, oracle_mod):
+    rng = random.Random(440)
+    m = bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
+    for lo, hi in [(10**9 - 1_000_000, 10**9 + 1_000_000), (3_000_000_000, 3_003_000_000)]:
+        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (lo, hi)
+
+
+def test_full_2p32_range(ctx):
+    """BASELINE configs[1] at full size: pinned by the C oracle (tests/golden/large.json),
+    then size-independent checks: shard invariance across 7 uneven shards and the
+    generic kernel on a 2^26 sub-range."""
+    import json
+    import os
+    from distributed_bitcoinminer_amd.parallel import merge
+    with open(os.path.join(os.path.dirname(__file__), "golden", "large.json")) as f:
+        case = json.load(f)[0]
+    m, lo, hi = bytes.fromhex(case["msg_hex"]), int(case["lo"]), int(case["hi"])
+    full = ctx.scan(m, lo, hi)
+    assert full == (int(case["hash"]), int(case["nonce"]))
+    assert _lib.host_hash(m, full[1]) == full[0]
+    cuts = [lo, 123_456_789, 10**9 - 1, 10**9 + 7, 2_000_000_001, 3_333_333_333, 4_000_000_000, hi + 1]
+    parts = [ctx.scan(m, a, b - 1) for a, b in zip(cuts, cuts[1:])]
+    assert merge(parts) == full
+
+
+def test_generic_vs_tiled_large(ctx):
+    lo, hi = 3 * 10**9, 3 * 10**9 + (1 << 26)
+    tiled = ctx.scan(b"bradfitz", lo, hi)
+    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+    try:
+        generic = ctx.scan(b"bradfitz", lo, hi)
+    finally:
+        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+    assert tiled == generic
