@@ -35,22 +35,50 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MSG = b"bradfitz"
 PER_GPU = 1 << 32
+
+
+def long120() -> bytes:
+    """BASELINE configs[2] message: random.Random(440), 120 chars 0x21..0x7e."""
+    import random
+    rng = random.Random(440)
+    return bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
+
+
+WORKLOADS = {
+    # name: (message, description)
+    "cfg2": (b"bradfitz", "cfg2: msg 'bradfitz' (8 B, C=1), 2^32 nonces per GPU "
+                          "[rank*2^32, (rank+1)*2^32), all-gather of 16-B candidates"),
+    "cfg3": (None, "cfg3: 120-B msg (random.Random(440)), C=2 (1 host-midstate block + 2 tail "
+                   "blocks), 2^32 nonces per GPU, all-gather of 16-B candidates"),
+}
+
+
+def profiled_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
+                       reverse=True):
+        with open(path) as f:
+            summ = json.load(f)
+        if kernel in summ:
+            return summ[kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
 OPS_PER_COMPRESSION = 1552           # SURVEY Appendix C
 PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T INT32 lane-ops/s
-CPU_SAMPLE = 12_000_000              # nonces for the 1-thread CPU baseline (~8-10 s)
+CPU_SAMPLE = 50_000_000              # nonces for the 1-thread CPU baseline (~12 s on the GPU box host)
 
 
-def cpu_baseline():
+def cpu_baseline(msg: bytes, name: str):
     from oracle import oracle
     oracle.build()
-    oracle.c_scan(MSG, 0, 100_000, threads=1)  # warm
+    oracle.c_scan(msg, 0, 100_000, threads=1)  # warm
     t = time.perf_counter()
-    oracle.c_scan(MSG, 0, CPU_SAMPLE - 1, threads=1)
+    oracle.c_scan(msg, 0, CPU_SAMPLE - 1, threads=1)
     dt = time.perf_counter() - t
     return {"value": CPU_SAMPLE / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
-            "sample": f"bradfitz nonces [0, {CPU_SAMPLE}) with oracle/hm_oracle.c "
+            "sample": f"{name} nonces [0, {CPU_SAMPLE}) with oracle/hm_oracle.c "
                       f"(Sprintf-style format + SHA-256 from the IV per nonce, strict <), "
                       f"1 thread; {dt:.2f} s",
             "mhs": CPU_SAMPLE / dt / 1e6}
@@ -62,7 +90,14 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
     args = ap.parse_args()
+    msg, desc = WORKLOADS[args.workload]
+    if msg is None:
+        msg = long120()
+    # Rehearsal on a 1-GPU box: HM_BENCH_BACKEND=gloo lets N ranks share GPU 0
+    # (RCCL refuses two ranks on one device).  The driver's runs use nccl.
+    backend = os.environ.get("HM_BENCH_BACKEND", "nccl")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -75,22 +110,27 @@ def main():
     from distributed_bitcoinminer_amd import _lib
     from distributed_bitcoinminer_amd.parallel import merge
 
+    gpu = local_rank if backend == "nccl" else 0
     dist = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
 
-    ctx = _lib.Context([local_rank])
+    ctx = _lib.Context([gpu])
     lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1
-    dev = torch.device("cuda", local_rank)
+    dev = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
+    cdev = torch.device("cuda", gpu)
     cand = torch.empty(2, dtype=torch.int64, device=dev)
     gathered = torch.empty(2 * world, dtype=torch.int64, device=dev)
 
     def step():
-        local = ctx.scan(MSG, lo, hi)
+        local = ctx.scan(msg, lo, hi)
         if world == 1:
             return local
         cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
@@ -101,7 +141,7 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(cdev)
 
     for _ in range(args.warmup):
         res = step()
@@ -109,7 +149,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-    torch.cuda.synchronize(dev)
+    torch.cuda.synchronize(cdev)
     barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
@@ -119,13 +159,18 @@ def main():
         elapsed = float(tt.item())
 
     # self-check: the winner re-hashes to the reported hash (host hm_hash)
-    assert _lib.host_hash(MSG, res[1]) == res[0], res
+    assert _lib.host_hash(msg, res[1]) == res[0], res
 
     if rank == 0:
         total = world * PER_GPU * args.steps
         value = total / elapsed / 1e9
         C = st["dom_compressions"]
-        achieved = st["dom_nonces"] * OPS_PER_COMPRESSION * C / (st["dom_kernel_ms"] * 1e-3) / 1e12
+        # per launch: algorithmic ops / average launch duration of the dominant kernel
+        launches = max(1, st["dom_launches"])
+        avg_ms = st["dom_kernel_ms"] / launches
+        ops_per_launch = st["dom_nonces"] / launches * OPS_PER_COMPRESSION * C
+        achieved = ops_per_launch / (avg_ms * 1e-3) / 1e12
+        traffic, traffic_src = profiled_traffic(st["dom_kernel"])
         line = {
             "metric": "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of INT32 VALU roofline",
             "value": round(value, 3),
@@ -138,22 +183,25 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (message 'bradfitz', contiguous nonce ranges; no dataset)",
-            "config": {"workload": "cfg2: msg 'bradfitz' (8 B, C=1), 2^32 nonces per GPU "
-                                   "[rank*2^32, (rank+1)*2^32), all-gather of 16-B candidates",
-                       "nonces_per_gpu": PER_GPU, "parallelism": f"dp{world} (nonce shards)"},
+            "data": "synthetic (fixed message, contiguous nonce ranges; no dataset)",
+            "config": {"workload": desc, "nonces_per_gpu": PER_GPU,
+                       "parallelism": f"dp{world} (nonce shards)",
+                       "merge": "RCCL all-gather" if world > 1 and backend == "nccl" else backend},
             "result": {"hash": res[0], "nonce": res[1]},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": round(PEAK_TOPS, 3), "unit": "T int32 lane-ops/s",
-                         "frac": round(achieved / PEAK_TOPS, 4), "traffic": None,
-                         "kernel": "hm_tiled_kernel (dominant launch)",
-                         "kernel_ms": round(st["dom_kernel_ms"], 3),
-                         "kernel_nonces": st["dom_nonces"],
+                         "frac": round(achieved / PEAK_TOPS, 4), "traffic": traffic,
+                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                         "traffic_source": traffic_src,
+                         "kernel": st["dom_kernel"],
+                         "launches_per_step": launches,
+                         "avg_launch_ms": round(avg_ms, 3),
+                         "nonces_per_launch": st["dom_nonces"] // launches,
                          "ops_per_nonce": OPS_PER_COMPRESSION * C,
                          "kernel_GHs": round(st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline()
+            cb = cpu_baseline(msg, args.workload)
             line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
         print(json.dumps(line), flush=True)
     ctx.close()

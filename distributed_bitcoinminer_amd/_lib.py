@@ -24,7 +24,7 @@ HM_ERR_RCCL = -5
 HM_ERR_INTERNAL = -6
 
 HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
-HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU = 1, 2, 3
+HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
 
 
 class HipMinerError(RuntimeError):
@@ -43,10 +43,14 @@ class hm_stats(ctypes.Structure):
                 ("dom_kernel_ms", ctypes.c_double), ("nonces", ctypes.c_uint64),
                 ("dom_nonces", ctypes.c_uint64), ("dom_compressions", ctypes.c_uint64),
                 ("launches", ctypes.c_int32), ("dom_kind", ctypes.c_int32),
-                ("ndev", ctypes.c_int32), ("dom_grid", ctypes.c_int32)]
+                ("ndev", ctypes.c_int32), ("dom_grid", ctypes.c_int32),
+                ("dom_launches", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("dom_kernel", ctypes.c_char * 64)]
 
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        d["dom_kernel"] = self.dom_kernel.decode()
+        return d
 
 
 _lib = None

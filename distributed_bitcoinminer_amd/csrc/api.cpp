@@ -22,6 +22,7 @@
 #include <chrono>
 #include <mutex>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "../../include/hipminer.h"
@@ -40,7 +41,13 @@ struct Launch {
     int kind;
     int grid;
     uint32_t compressions;
+    char kernel[64];  // kernel instantiation, as rocprofv3 names it (sans args)
 };
+
+void name_tiled(char* out, const SegPlan& s) {
+    snprintf(out, 64, "hm_tiled_kernel<%d, %s, %s>", s.W1, s.straddle ? "true" : "false",
+             s.trailer ? "true" : "false");
+}
 
 struct Device {
     int ordinal = -1;
@@ -85,6 +92,7 @@ struct hm_ctx {
     bool force_generic = false;
     bool merge_rccl = false;
     int grid_per_cu = 0;
+    int streams = 1;
     bool have_stats = false;
     hm_stats last{};
 };
@@ -213,6 +221,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         if (rc) return rc;
         L.nonces = tile_span_nonces(s, t, nt);
         L.kind = HM_KIND_CHAINED;
+        snprintf(L.kernel, sizeof L.kernel, "hm_chained_kernel");
         L.grid = grid;
         L.compressions = count_compressions(s);
         HIPCHK(hipEventRecord(L.start, st));
@@ -277,6 +286,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             if (rc) return rc;
             L.nonces = tile_span_nonces(s, t, nt);
             L.kind = HM_KIND_TILED;
+            name_tiled(L.kernel, s);
             L.grid = grid;
             L.compressions = count_compressions(s);
             HIPCHK(hipEventRecord(L.start, st));
@@ -311,6 +321,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     if (rc) return rc;
     L.nonces = ga.count_m1 + 1;  // generic segments are far below 2^64
     L.kind = HM_KIND_GENERIC;
+    snprintf(L.kernel, sizeof L.kernel, "hm_generic_kernel");
     L.grid = grid;
     L.compressions = count_compressions(s);
     HIPCHK(hipEventRecord(L.start, st));
@@ -334,14 +345,17 @@ int enqueue_device_scan(hm_ctx* ctx, Device& dv, const MsgPlan& mp, uint64_t lo,
     HIPCHK(hipEventRecord(dv.join[0], s0));
     for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
     std::vector<SegPlan> segs = plan_range(mp, lo, hi, ctx->force_generic);
-    // the largest segment on stream 0, the rest spread over streams 1..
+    // streams == 1 (default): every segment in order on stream 0, so kernels
+    // never overlap and per-kernel timings match rocprofv3.  streams > 1: the
+    // largest segment on stream 0, the rest spread over streams 1..
+    const int nstreams = std::max(1, std::min(ctx->streams, kStreams));
     size_t big = 0;
     for (size_t i = 1; i < segs.size(); ++i)
         if (segs[i].hi - segs[i].lo > segs[big].hi - segs[big].lo) big = i;
     int rr = 0;
     for (size_t i = 0; i < segs.size(); ++i) {
         int si = 0;
-        if (i != big) si = 1 + (rr++ % (kStreams - 1));
+        if (nstreams > 1 && i != big) si = 1 + (rr++ % (nstreams - 1));
         int rc = enqueue_segment(ctx, dv, mp, segs[i], si);
         if (rc) return rc;
     }
@@ -457,6 +471,10 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
     switch (opt) {
         case HM_OPT_FORCE_GENERIC: ctx->force_generic = value != 0; return HM_OK;
         case HM_OPT_MERGE_RCCL: ctx->merge_rccl = value != 0; return HM_OK;
+        case HM_OPT_STREAMS:
+            if (value < 1 || value > kStreams) return HM_ERR_INVALID;
+            ctx->streams = (int)value;
+            return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;
             ctx->grid_per_cu = (int)value;
@@ -524,19 +542,37 @@ int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t h
     hm_stats st{};
     st.ndev = n;
     st.nonces = empty ? 0 : span_m1 + 1;  // wraps to 0 for the full 2^64 range
+    // aggregate per kernel instantiation; the dominant one has the most nonces
+    struct Agg { std::string name; double ms = 0; uint64_t nonces = 0; int launches = 0;
+                 int kind = 0, grid = 0; uint32_t comp = 0; uint64_t big = 0; };
+    std::vector<Agg> aggs;
     for (auto& dv : ctx->devs) {
         for (auto& L : dv.launches) {
             float ms = 0.f;
             HIPCHK(hipEventElapsedTime(&ms, L.start, L.stop));
             st.kernel_ms += ms;
             st.launches += 1;
-            if (L.nonces > st.dom_nonces) {
-                st.dom_nonces = L.nonces;
-                st.dom_kernel_ms = ms;
-                st.dom_compressions = L.compressions;
-                st.dom_kind = L.kind;
-                st.dom_grid = L.grid;
-            }
+            Agg* a = nullptr;
+            for (auto& x : aggs)
+                if (x.name == L.kernel) a = &x;
+            if (!a) { aggs.push_back(Agg{}); a = &aggs.back(); a->name = L.kernel; }
+            a->ms += ms;
+            a->nonces += L.nonces;
+            a->launches += 1;
+            a->kind = L.kind;
+            a->comp = std::max(a->comp, L.compressions);
+            if (L.nonces > a->big) { a->big = L.nonces; a->grid = L.grid; }
+        }
+    }
+    for (auto& a : aggs) {
+        if (a.nonces > st.dom_nonces) {
+            st.dom_nonces = a.nonces;
+            st.dom_kernel_ms = a.ms;
+            st.dom_compressions = a.comp;
+            st.dom_kind = a.kind;
+            st.dom_grid = a.grid;
+            st.dom_launches = a.launches;
+            snprintf(st.dom_kernel, sizeof st.dom_kernel, "%s", a.name.c_str());
         }
     }
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)

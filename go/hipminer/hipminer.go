@@ -1,0 +1,98 @@
+// Package hipminer is the cgo binding of libhipminer.so (include/hipminer.h):
+// the MI355X backend for the min-hash scan of the reference miner
+// (cmu440/bitcoin/miner/miner.go:63-76, bitcoin.Hash at
+// cmu440/bitcoin/hash.go:13-17).
+//
+// Built only where a Go toolchain exists (none in the build image); the C ABI
+// it binds is tested from Python/ctypes in tests/.
+package hipminer
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../distributed_bitcoinminer_amd -lhipminer -Wl,-rpath,${SRCDIR}/../../distributed_bitcoinminer_amd
+#include <stdlib.h>
+#include "hipminer.h"
+*/
+import "C"
+
+import (
+	"fmt"
+	"unsafe"
+)
+
+const maxUint64 = ^uint64(0)
+
+// Error carries an hm_* return code.
+type Error struct{ Code int }
+
+func (e Error) Error() string {
+	return fmt.Sprintf("hipminer: %s (rc=%d)", C.GoString(C.hm_strerror(C.int(e.Code))), e.Code)
+}
+
+// Miner owns one hm_ctx (device buffers, streams).  Safe for concurrent use:
+// the library serialises calls per context and re-binds the device on every
+// call, so Go may run them on any OS thread.
+type Miner struct{ ctx *C.hm_ctx }
+
+// Open binds the given HIP device ordinals; none means every visible device.
+func Open(devices ...int) (*Miner, error) {
+	var ctx *C.hm_ctx
+	var rc C.int
+	if len(devices) == 0 {
+		rc = C.hm_open(nil, 0, &ctx)
+	} else {
+		ds := make([]C.int, len(devices))
+		for i, d := range devices {
+			ds[i] = C.int(d)
+		}
+		rc = C.hm_open(&ds[0], C.int(len(ds)), &ctx)
+	}
+	if rc != 0 {
+		return nil, Error{int(rc)}
+	}
+	return &Miner{ctx: ctx}, nil
+}
+
+// ScanInclusive returns the lexicographic min of (Hash(data, n), n) over the
+// inclusive range [lo, hi]; (MaxUint64, 0) when lo > hi.
+func (m *Miner) ScanInclusive(data string, lo, hi uint64) (hash, nonce uint64, err error) {
+	var out C.hm_result
+	var p *C.uint8_t
+	if len(data) > 0 {
+		// Borrowed for the call only; the bytes hold no Go pointers (cgo rules).
+		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
+	}
+	rc := C.hm_scan(m.ctx, p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi), &out)
+	if rc != 0 {
+		return 0, 0, Error{int(rc)}
+	}
+	return uint64(out.hash), uint64(out.nonce), nil
+}
+
+// EvalRequest is the drop-in for miner.go:63-76: it keeps the reference's
+// `upper := Upper + 1` uint64 wrap (Upper == MaxUint64 scans nothing) and
+// its initial (MaxUint64, 0).
+func (m *Miner) EvalRequest(data string, lower, upper uint64) (hash, nonce uint64, err error) {
+	end := upper + 1 // wraps exactly like miner.go:69
+	if !(lower < end) {
+		return maxUint64, 0, nil
+	}
+	return m.ScanInclusive(data, lower, end-1)
+}
+
+// Close releases the context.
+func (m *Miner) Close() {
+	if m.ctx != nil {
+		C.hm_close(m.ctx)
+		m.ctx = nil
+	}
+}
+
+// Hash is bitcoin.Hash(msg, nonce) computed by the library on the host.
+func Hash(msg string, nonce uint64) uint64 {
+	var p *C.uint8_t
+	if len(msg) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(msg)))
+	}
+	return uint64(C.hm_hash(p, C.size_t(len(msg)), C.uint64_t(nonce)))
+}

@@ -60,16 +60,21 @@ typedef struct hm_ctx hm_ctx;
 typedef struct hm_stats {
     double wall_ms;          /* host wall time of the hm_scan call              */
     double kernel_ms;        /* sum of scan-kernel durations (HIP events)        */
-    double dom_kernel_ms;    /* duration of the dominant (largest) scan launch   */
+    double dom_kernel_ms;    /* summed duration of the dominant scan kernel's
+                                launches (dominant = most nonces; one kernel
+                                instantiation may serve several segments)       */
     uint64_t nonces;         /* nonces covered by the call                       */
-    uint64_t dom_nonces;     /* nonces covered by the dominant launch            */
+    uint64_t dom_nonces;     /* nonces covered by the dominant kernel            */
     uint64_t dom_compressions; /* SHA-256 compressions per nonce after the host
-                                  midstate in the dominant launch (C of SURVEY
-                                  §8d; algorithmic, before any hoisting)         */
+                                  midstate in the dominant kernel's segments (C
+                                  of SURVEY §8d; algorithmic, before hoisting)  */
     int32_t launches;        /* scan-kernel launches issued                      */
-    int32_t dom_kind;        /* HM_KIND_* of the dominant launch                 */
+    int32_t dom_kind;        /* HM_KIND_* of the dominant kernel                 */
     int32_t ndev;            /* devices used                                      */
-    int32_t dom_grid;        /* workgroups of the dominant launch                */
+    int32_t dom_grid;        /* workgroups of the dominant kernel's largest launch */
+    int32_t dom_launches;    /* launches of the dominant kernel                  */
+    int32_t reserved;
+    char dom_kernel[64];     /* its name as rocprofv3 lists it (without args)   */
 } hm_stats;
 
 #define HM_OK 0
@@ -89,6 +94,8 @@ typedef struct hm_stats {
 #define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */
 #define HM_OPT_MERGE_RCCL 2    /* 1: merge multi-device candidates with RCCL     */
 #define HM_OPT_GRID_PER_CU 3   /* workgroups per CU for scan launches (0 = auto) */
+#define HM_OPT_STREAMS 4       /* HIP streams per device for segment launches
+                                  (1..4, default 1 = serial, clean profiles)   */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */

@@ -89,11 +89,12 @@ def test_chained_layouts_vs_oracle(ctx, oracle_mod):
             T = r + d
             if T < 65 or T - 64 > 4:
                 continue
-            seg = [s for s in _lib.debug_plan(m, 10**(d - 1), 10**d - 1)][0]
+            dhi = min(10**d - 1, MAX)
+            seg = _lib.debug_plan(m, 10**(d - 1), dhi)[0]
             if seg["kind"] != _lib.HM_KIND_CHAINED:
                 continue
             seen.add((T - 64, seg["V"] - (T - 64)))
-            base = rng.randrange(10**(d - 1), 10**d - 300_000)
+            base = rng.randrange(10**(d - 1), dhi - 300_000)
             lo, hi = base, base + rng.randrange(1, 250_000)
             assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
     assert {(1, 4), (2, 4), (3, 4), (4, 4)} <= seen
@@ -133,3 +134,51 @@ def test_generic_vs_tiled_large(ctx):
     finally:
         ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
     assert tiled == generic
+
+
+def test_options_streams_and_rccl_merge(oracle_mod):
+    """Multi-stream segment overlap and the RCCL candidate merge (1-device
+    communicator on this box) give the same answer as the default path."""
+    lo, hi = 10**8 - 3_000_000, 10**8 + 3_000_000  # 8- and 9-digit segments
+    exp = oracle_mod.c_scan(b"jonny greenwood", lo, hi)
+    with _lib.Context([0]) as c:
+        c.set_option(_lib.HM_OPT_STREAMS, 4)
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        c.set_option(_lib.HM_OPT_GRID_PER_CU, 1)
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+    with _lib.Context() as c:  # every visible device
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+
+
+def test_miner_eval_request_on_gpu(ctx, golden):
+    from distributed_bitcoinminer_amd import bitcoin, miner
+    mnr = miner.Miner(ctx=ctx)
+    for k in golden["miner_eval_kats"]:
+        req = bitcoin.NewRequest(bytes.fromhex(k["msg_hex"]), int(k["lower"]), int(k["upper"]))
+        out, err = bitcoin.unmarshal(mnr.eval_request(bitcoin.marshal(req)))
+        assert err is None and (out.Hash, out.Nonce) == (int(k["hash"]), int(k["nonce"]))
+
+
+def test_stats_accounting(ctx):
+    ctx.scan(b"bradfitz", 0, 2**32 - 1)
+    st = ctx.stats()
+    assert st["nonces"] == 2**32
+    assert st["dom_kernel"] == "hm_tiled_kernel<4, false, false>"
+    assert st["dom_nonces"] == 900_000_000 + 2**32 - 10**9 and st["dom_launches"] == 2
+    assert st["dom_compressions"] == 1 and st["dom_kind"] == _lib.HM_KIND_TILED
+    assert 0 < st["dom_kernel_ms"] <= st["kernel_ms"] <= st["wall_ms"] * 1.5
+
+
+def test_server_model_end_to_end_gpu(ctx, oracle_mod):
+    """Config-5 style: 8 GPU 'miners' (one context, eight chunk requests) under the
+    server's chunking near 2^64-1; the last chunk ends at 2^64-1 and scans nothing."""
+    from distributed_bitcoinminer_amd import miner, server_model as sm
+    mnr = miner.Miner(ctx=ctx)
+    for msg in (b"bradfitz", b"thom yorke", b"jonny greenwood"):
+        lo, up = MAX - 1 - 4_000_000, MAX - 1
+        got = sm.expected_client_result(msg, lo, up, 8, mnr.scan)
+        chunks = sm.load_balance(lo, up, 8)
+        assert chunks[-1][1] == MAX
+        assert got == oracle_mod.c_scan(msg, lo, chunks[-1][0])
