@@ -74,14 +74,15 @@ def cpu_baseline(msg: bytes, name: str):
     from oracle import oracle
     oracle.build()
     oracle.c_scan(msg, 0, 100_000, threads=1)  # warm
+    n = CPU_SAMPLE if len(msg) + 21 <= 55 else CPU_SAMPLE // 3  # 1 vs 3 compressions per nonce
     t = time.perf_counter()
-    oracle.c_scan(msg, 0, CPU_SAMPLE - 1, threads=1)
+    oracle.c_scan(msg, 0, n - 1, threads=1)
     dt = time.perf_counter() - t
-    return {"value": CPU_SAMPLE / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
-            "sample": f"{name} nonces [0, {CPU_SAMPLE}) with oracle/hm_oracle.c "
+    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
+            "sample": f"{name} nonces [0, {n}) with oracle/hm_oracle.c "
                       f"(Sprintf-style format + SHA-256 from the IV per nonce, strict <), "
                       f"1 thread; {dt:.2f} s",
-            "mhs": CPU_SAMPLE / dt / 1e6}
+            "mhs": n / dt / 1e6}
 
 
 def main():
