@@ -1,0 +1,90 @@
+"""End to end on the GPU: native hm_miner processes join an LSP server and
+answer Requests, as the staff `mtest` checks a miner (p1/README.md:139-141),
+and several miners under the reference server's chunking/merge model
+(server.go:165-205, 273-276; config-5 style, near 2^64-1)."""
+import os
+import subprocess
+
+import pytest
+
+from distributed_bitcoinminer_amd import bitcoin, server_model as sm
+from tests import lsp_harness as H
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MINER = os.path.join(ROOT, "distributed_bitcoinminer_amd", "hm_miner")
+MAX = (1 << 64) - 1
+ENV = dict(os.environ, HM_LSP_EPOCH_MS="100", HM_LSP_EPOCH_LIMIT="50", HIPMINER_DEVICES="0")
+
+
+def _spawn(srv):
+    assert os.path.exists(MINER), "build hm_miner first (__graft_entry__.build())"
+    return subprocess.Popen([MINER, srv.hostport], env=ENV, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+
+
+def _ask(srv, cid, data, lower, upper):
+    srv.write(cid, bitcoin.marshal(bitcoin.NewRequest(data, lower, upper)))
+    res, err = bitcoin.unmarshal(srv.read(cid, timeout=120))
+    assert err is None and res.Type == bitcoin.Result
+    return res.Hash, res.Nonce
+
+
+def test_miner_join_and_requests(oracle_mod, golden):
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=50)
+    p = _spawn(srv)
+    try:
+        cid = srv.accept(timeout=120)
+        assert srv.read(cid, timeout=60) == bitcoin.marshal(bitcoin.NewJoin())
+        # config 1 through the server: client maxNonce 10^7 -> miner Request [0, 10^7+1]
+        assert _ask(srv, cid, "bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+        for k in golden["miner_eval_kats"]:
+            exp = (int(k["hash"]), int(k["nonce"]))
+            assert _ask(srv, cid, bytes.fromhex(k["msg_hex"]), int(k["lower"]), int(k["upper"])) == exp
+        m = "thom yorke".encode()
+        assert _ask(srv, cid, m, 19970000, 19971000) == oracle_mod.c_scan(m, 19970000, 19971000)
+        weird = 'a<b>&"é '.encode()
+        assert _ask(srv, cid, weird, 5, 5000) == oracle_mod.c_scan(weird, 5, 5000)
+    finally:
+        srv.close()
+        try:
+            p.wait(timeout=60)  # loses the server after EpochLimit epochs and exits
+        except subprocess.TimeoutExpired:
+            p.kill()
+    assert p.returncode == 0, p.stderr.read() if p.stderr else ""
+
+
+def test_three_miners_under_server_model(oracle_mod):
+    """Three GPU miner processes; the fake server splits each client request the
+    way server.go:165-205 does and merges in arrival order (:273-276)."""
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=50)
+    procs = [_spawn(srv) for _ in range(3)]
+    try:
+        cids = [srv.accept(timeout=120) for _ in procs]
+        for c in cids:
+            assert srv.read(c, timeout=60) == bitcoin.marshal(bitcoin.NewJoin())
+        reqs = [(b"bradfitz", MAX - 1 - 3_000_000, MAX - 1),
+                (b"jonny greenwood", 0, 9999),
+                (b"thom yorke", 10**19, 10**19 + 2_000_000)]
+        for data, lo, up in reqs:
+            chunks = sm.load_balance(lo, up, len(cids))
+            for c, (a, b) in zip(cids, chunks):
+                srv.write(c, bitcoin.marshal(bitcoin.NewRequest(data, a, b)))
+            results = []
+            for c, _ in zip(cids, chunks):
+                r, _ = bitcoin.unmarshal(srv.read(c, timeout=120))
+                results.append((r.Hash, r.Nonce))
+            got = sm.merge_in_arrival_order(results)
+            # expected: the union of what the miners scan (the last chunk of the
+            # near-2^64 request ends at 2^64-1 and scans nothing)
+            exp = sm.expected_client_result(
+                data, lo, up, len(cids),
+                lambda d, a, b: oracle_mod.c_miner_eval(d, a, b))
+            assert got == exp, (data, lo, up)
+    finally:
+        srv.close()
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
