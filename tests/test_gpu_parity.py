@@ -182,3 +182,47 @@ def test_server_model_end_to_end_gpu(ctx, oracle_mod):
         chunks = sm.load_balance(lo, up, 8)
         assert chunks[-1][1] == MAX
         assert got == oracle_mod.c_scan(msg, lo, chunks[-1][0])
+
+
+def test_layout_sweep_segment_edges(ctx, oracle_mod):
+    """Every message length 0..130 x every digit count: small ranges at both
+    ends of each digit segment (partial tiles, masking, digit-count changes)."""
+    import random as _r
+    rng = _r.Random(31)
+    for L in range(0, 131):
+        m = bytes(rng.randrange(256) for _ in range(L))
+        for d in range(1, 21):
+            dlo = 0 if d == 1 else 10**(d - 1)
+            dhi = min(10**d - 1, MAX)
+            for lo, hi in ((dlo, min(dhi, dlo + 700)), (max(dlo, dhi - 700), min(MAX, dhi + 300))):
+                assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
+
+
+def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
+    """Whole tiles (10^5..10^8 nonces) of every layout the planner picks for
+    lengths 0..130: fast kernels vs the independent generic kernel."""
+    import random as _r
+    rng = _r.Random(77)
+    seen = set()
+    for L in range(0, 131):
+        m = bytes(rng.randrange(32, 127) for _ in range(L))
+        for d in (7, 8, 10, 12, 16, 20):
+            dlo, dhi = 10**(d - 1), min(10**d - 1, MAX)
+            seg = _lib.debug_plan(m, dlo, dhi)[0]
+            if seg["kind"] == _lib.HM_KIND_GENERIC:
+                continue
+            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"])
+            if key in seen:
+                continue
+            seen.add(key)
+            span = min(2 * 10**seg["V"] + 12345, 3 * 10**8, (dhi - dlo) // 2)
+            lo = rng.randrange(dlo, dhi - span)
+            fast = ctx.scan(m, lo, lo + span)
+            ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+            try:
+                slow = ctx.scan(m, lo, lo + span)
+            finally:
+                ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+            assert fast == slow, (L, d, key)
+            assert _lib.host_hash(m, fast[1]) == fast[0]
+    assert len(seen) >= 40, len(seen)
