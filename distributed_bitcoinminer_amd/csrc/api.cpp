@@ -497,7 +497,6 @@ int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t h
     const uint64_t span_m1 = empty ? 0 : hi - lo;
     const uint64_t q = span_m1 / (uint64_t)n, rr = span_m1 % (uint64_t)n;
     uint64_t start = lo;
-    std::vector<bool> dev_empty(n, empty);
     for (int i = 0; i < n; ++i) {
         uint64_t a = 0, b = 0;
         bool e = empty;
@@ -508,7 +507,6 @@ int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t h
             b = start + cnt_m1;
             if (!e) start = b + 1;
         }
-        dev_empty[i] = e;
         int rc = enqueue_device_scan(ctx, ctx->devs[i], mp, a, b, e);
         if (rc) return rc;
     }
