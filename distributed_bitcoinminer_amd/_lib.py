@@ -38,6 +38,11 @@ class hm_result(ctypes.Structure):
     _fields_ = [("hash", ctypes.c_uint64), ("nonce", ctypes.c_uint64)]
 
 
+class hm_request(ctypes.Structure):
+    _fields_ = [("msg", ctypes.c_char_p), ("len", ctypes.c_size_t),
+                ("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
 class hm_stats(ctypes.Structure):
     _fields_ = [("wall_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
                 ("dom_kernel_ms", ctypes.c_double), ("nonces", ctypes.c_uint64),
@@ -80,6 +85,9 @@ def load() -> ctypes.CDLL:
         lib.hm_scan.restype = ctypes.c_int
         lib.hm_scan.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.c_uint64,
                                 ctypes.c_uint64, ctypes.POINTER(hm_result)]
+        lib.hm_scan_many.restype = ctypes.c_int
+        lib.hm_scan_many.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_request), ctypes.c_int,
+                                     ctypes.POINTER(hm_result)]
         lib.hm_scan_stats.restype = ctypes.c_int
         lib.hm_scan_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats)]
         lib.hm_set_option.restype = ctypes.c_int
@@ -136,6 +144,20 @@ class Context:
         if rc != HM_OK:
             raise HipMinerError(rc, "hm_scan")
         return int(out.hash), int(out.nonce)
+
+    def scan_many(self, requests) -> list[tuple[int, int]]:
+        """hm_scan_many over [(msg, lo, hi), ...]."""
+        reqs = list(requests)
+        n = len(reqs)
+        keep = [as_bytes(m) for m, _, _ in reqs]
+        arr = (hm_request * max(1, n))()
+        for i, ((_, lo, hi), m) in enumerate(zip(reqs, keep)):
+            arr[i] = hm_request(m, len(m), lo, hi)
+        outs = (hm_result * max(1, n))()
+        rc = self._lib.hm_scan_many(self._h, arr, n, outs)
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_scan_many")
+        return [(int(outs[i].hash), int(outs[i].nonce)) for i in range(n)]
 
     def stats(self) -> dict:
         st = hm_stats()

@@ -57,10 +57,10 @@ struct Device {
     uint32_t* kwt[kStreams] = {};
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
-    uint64_t* best = nullptr;      // [kStreams][2]
-    uint64_t* result = nullptr;    // [2]
-    uint64_t* gathered = nullptr;  // [2 * ndev] (RCCL merge)
-    hm_result* host_out = nullptr; // pinned
+    uint64_t* best = nullptr;      // [kMaxBatch][kStreams][2]: per request, per stream
+    uint64_t* result = nullptr;    // [kMaxBatch][2]
+    uint64_t* gathered = nullptr;  // [ndev][kMaxBatch][2] (RCCL merge)
+    hm_result* host_out = nullptr; // pinned [kMaxBatch]
     hipEvent_t join[kStreams] = {};
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
@@ -123,9 +123,9 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
     }
-    HIPCHK(hipMalloc(&dv.best, kStreams * 2 * sizeof(uint64_t)));
-    HIPCHK(hipMalloc(&dv.result, 2 * sizeof(uint64_t)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), sizeof(hm_result)));
+    HIPCHK(hipMalloc(&dv.best, (size_t)kMaxBatch * kStreams * 2 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&dv.result, (size_t)kMaxBatch * 2 * sizeof(uint64_t)));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), kMaxBatch * sizeof(hm_result)));
     return HM_OK;
 }
 
@@ -175,7 +175,8 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
-int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si) {
+int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si,
+                    uint64_t* best) {
     hipStream_t st = dv.stream[si];
     HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.total_bits, st));
     const uint64_t per_tile = (uint64_t)s.tpt * s.ntc;
@@ -227,7 +228,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         HIPCHK(hipEventRecord(L.start, st));
         HIPCHK(launch_chained(ca, grid, st));
         HIPCHK(hipEventRecord(L.stop, st));
-        HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), dv.best + 2 * si,
+        HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si,
                            st));
         dv.launches.push_back(L);
         t += nt;
@@ -237,9 +238,11 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
 }
 
 // Enqueue one segment on stream `si`; records its launches for stats.
-int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si) {
+// `best` = the request's [kStreams][2] running bests; this stream folds into best + 2*si.
+int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si,
+                    uint64_t* best) {
     hipStream_t st = dv.stream[si];
-    if (s.kind == HM_KIND_CHAINED) return enqueue_chained(ctx, dv, mp, s, si);
+    if (s.kind == HM_KIND_CHAINED) return enqueue_chained(ctx, dv, mp, s, si, best);
     if (s.kind == HM_KIND_TILED) {
         uint32_t kw[64] = {0};
         if (s.trailer) trailer_kw(s, kw);
@@ -293,7 +296,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             HIPCHK(launch_tiled(ta, s.W1, s.straddle, s.trailer, grid, st));
             HIPCHK(hipEventRecord(L.stop, st));
             HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize),
-                               dv.best + 2 * si, st));
+                               best + 2 * si, st));
             dv.launches.push_back(L);
             t += nt;
             if (t == 0) break;  // tile index wrapped (cannot happen for d <= 20)
@@ -327,43 +330,53 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     HIPCHK(hipEventRecord(L.start, st));
     HIPCHK(launch_generic(ga, grid, st));
     HIPCHK(hipEventRecord(L.stop, st));
-    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), dv.best + 2 * si, st));
+    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si, st));
     dv.launches.push_back(L);
     return HM_OK;
 }
 
-// Enqueue the whole scan of [lo, hi] on one device; result lands in dv.result.
-int enqueue_device_scan(hm_ctx* ctx, Device& dv, const MsgPlan& mp, uint64_t lo, uint64_t hi,
-                        bool empty) {
+struct DevReq {
+    const MsgPlan* mp;
+    uint64_t lo, hi;
+    bool empty;
+};
+
+// Enqueue a batch of scans on one device; request r's result lands in
+// dv.result + 2r.  All segments of all requests are queued before any sync.
+int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& reqs) {
     HIPCHK(hipSetDevice(dv.ordinal));
-    dv.evnext = 0;
-    dv.launches.clear();
+    const int n = (int)reqs.size();
     hipStream_t s0 = dv.stream[0];
-    HIPCHK(launch_init_best(dv.best, kStreams, s0));
-    HIPCHK(launch_init_best(dv.result, 1, s0));
-    if (empty) return HM_OK;
+    HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
+    HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
     HIPCHK(hipEventRecord(dv.join[0], s0));
     for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
-    std::vector<SegPlan> segs = plan_range(mp, lo, hi, ctx->force_generic);
     // streams == 1 (default): every segment in order on stream 0, so kernels
     // never overlap and per-kernel timings match rocprofv3.  streams > 1: the
-    // largest segment on stream 0, the rest spread over streams 1..
+    // largest segment of each request on stream 0, the rest spread over 1..
     const int nstreams = std::max(1, std::min(ctx->streams, kStreams));
-    size_t big = 0;
-    for (size_t i = 1; i < segs.size(); ++i)
-        if (segs[i].hi - segs[i].lo > segs[big].hi - segs[big].lo) big = i;
     int rr = 0;
-    for (size_t i = 0; i < segs.size(); ++i) {
-        int si = 0;
-        if (nstreams > 1 && i != big) si = 1 + (rr++ % (nstreams - 1));
-        int rc = enqueue_segment(ctx, dv, mp, segs[i], si);
-        if (rc) return rc;
+    for (int r = 0; r < n; ++r) {
+        if (reqs[r].empty) continue;
+        std::vector<SegPlan> segs = plan_range(*reqs[r].mp, reqs[r].lo, reqs[r].hi,
+                                               ctx->force_generic);
+        size_t big = 0;
+        for (size_t i = 1; i < segs.size(); ++i)
+            if (segs[i].hi - segs[i].lo > segs[big].hi - segs[big].lo) big = i;
+        uint64_t* best = dv.best + (size_t)r * kStreams * 2;
+        for (size_t i = 0; i < segs.size(); ++i) {
+            int si = 0;
+            if (nstreams > 1 && i != big) si = 1 + (rr++ % (nstreams - 1));
+            int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], si, best);
+            if (rc) return rc;
+        }
     }
     for (int s = 1; s < kStreams; ++s) {
         HIPCHK(hipEventRecord(dv.join[s], dv.stream[s]));
         HIPCHK(hipStreamWaitEvent(s0, dv.join[s], 0));
     }
-    HIPCHK(launch_fold(dv.best, kStreams, dv.result, s0));
+    for (int r = 0; r < n; ++r)
+        HIPCHK(launch_fold(dv.best + (size_t)r * kStreams * 2, kStreams, dv.result + 2 * r, s0));
     return HM_OK;
 }
 
@@ -371,7 +384,8 @@ bool lex_less(uint64_t k1, uint64_t n1, uint64_t k2, uint64_t n2) {
     return k1 < k2 || (k1 == k2 && n1 < n2);
 }
 
-int rccl_merge(hm_ctx* ctx) {
+// All-gather every device's n 16-B results over RCCL; device 0 folds them.
+int rccl_merge(hm_ctx* ctx, int nreq) {
     const int n = (int)ctx->devs.size();
     if (!ctx->devs[0].comm) {
         std::vector<ncclComm_t> comms(n);
@@ -381,25 +395,88 @@ int rccl_merge(hm_ctx* ctx) {
         for (int i = 0; i < n; ++i) {
             ctx->devs[i].comm = comms[i];
             HIPCHK(hipSetDevice(ctx->devs[i].ordinal));
-            HIPCHK(hipMalloc(&ctx->devs[i].gathered, (size_t)n * 2 * sizeof(uint64_t)));
+            HIPCHK(hipMalloc(&ctx->devs[i].gathered, (size_t)n * kMaxBatch * 2 * sizeof(uint64_t)));
         }
     }
     if (ncclGroupStart() != ncclSuccess) return HM_ERR_RCCL;
     for (int i = 0; i < n; ++i) {
         Device& dv = ctx->devs[i];
         HIPCHK(hipSetDevice(dv.ordinal));
-        if (ncclAllGather(dv.result, dv.gathered, 2, ncclUint64, dv.comm, dv.stream[0]) !=
-            ncclSuccess) {
+        if (ncclAllGather(dv.result, dv.gathered, (size_t)2 * nreq, ncclUint64, dv.comm,
+                          dv.stream[0]) != ncclSuccess) {
             ncclGroupEnd();
             return HM_ERR_RCCL;
         }
     }
     if (ncclGroupEnd() != ncclSuccess) return HM_ERR_RCCL;
-    // every rank now holds all candidates; rank 0 folds them
+    // gathered[d][r][2]: request r's candidates are strided by nreq pairs
     Device& d0 = ctx->devs[0];
     HIPCHK(hipSetDevice(d0.ordinal));
-    HIPCHK(launch_init_best(d0.result, 1, d0.stream[0]));
-    HIPCHK(launch_fold(d0.gathered, (uint32_t)n, d0.result, d0.stream[0]));
+    HIPCHK(launch_init_best(d0.result, (uint32_t)nreq, d0.stream[0]));
+    for (int r = 0; r < nreq; ++r)
+        HIPCHK(launch_fold(d0.gathered + 2 * r, (uint32_t)n, d0.result + 2 * r, d0.stream[0],
+                           (uint32_t)nreq));
+    return HM_OK;
+}
+
+// One chunk (<= kMaxBatch requests) of hm_scan_many.
+int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
+    const int ndev = (int)ctx->devs.size();
+    std::vector<MsgPlan> plans(nreq);
+    std::vector<std::vector<DevReq>> per_dev(ndev, std::vector<DevReq>(nreq));
+    static const uint8_t empty_msg = 0;
+    for (int r = 0; r < nreq; ++r) {
+        const hm_request& q = reqs[r];
+        plans[r] = plan_message(q.msg ? q.msg : &empty_msg, q.msg ? q.len : 0);
+        const bool empty = q.lo > q.hi;
+        // contiguous shards: span_m1 + 1 = ndev*qq + (rr + 1); shards 0..rr get qq+1
+        const uint64_t span_m1 = empty ? 0 : q.hi - q.lo;
+        const uint64_t qq = span_m1 / (uint64_t)ndev, rr = span_m1 % (uint64_t)ndev;
+        uint64_t start = q.lo;
+        for (int i = 0; i < ndev; ++i) {
+            DevReq& dr = per_dev[i][r];
+            dr.mp = &plans[r];
+            dr.empty = empty || (qq == 0 && (uint64_t)i > rr);
+            dr.lo = dr.hi = 0;
+            if (!dr.empty) {
+                const uint64_t cnt_m1 = qq - 1u + ((uint64_t)i <= rr ? 1u : 0u);  // modular
+                dr.lo = start;
+                dr.hi = start + cnt_m1;
+                start = dr.hi + 1;
+            }
+        }
+    }
+    for (int i = 0; i < ndev; ++i) {
+        int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i]);
+        if (rc) return rc;
+    }
+    if (ndev > 1 && ctx->merge_rccl) {
+        int rc = rccl_merge(ctx, nreq);
+        if (rc) return rc;
+        Device& d0 = ctx->devs[0];
+        HIPCHK(hipSetDevice(d0.ordinal));
+        HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, nreq * sizeof(hm_result),
+                              hipMemcpyDeviceToHost, d0.stream[0]));
+        for (auto& dv : ctx->devs) {
+            HIPCHK(hipSetDevice(dv.ordinal));
+            HIPCHK(hipStreamSynchronize(dv.stream[0]));
+        }
+        for (int r = 0; r < nreq; ++r) outs[r] = d0.host_out[r];
+        return HM_OK;
+    }
+    for (auto& dv : ctx->devs) {
+        HIPCHK(hipSetDevice(dv.ordinal));
+        HIPCHK(hipMemcpyAsync(dv.host_out, dv.result, nreq * sizeof(hm_result),
+                              hipMemcpyDeviceToHost, dv.stream[0]));
+    }
+    for (int r = 0; r < nreq; ++r) outs[r] = hm_result{~0ull, 0};
+    for (auto& dv : ctx->devs) {
+        HIPCHK(hipSetDevice(dv.ordinal));
+        HIPCHK(hipStreamSynchronize(dv.stream[0]));
+        for (int r = 0; r < nreq; ++r)
+            if (lex_less(dv.host_out[r].hash, dv.host_out[r].nonce, outs[r].hash, outs[r].nonce))
+                outs[r] = dv.host_out[r];
+    }
     return HM_OK;
 }
 
@@ -483,63 +560,30 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
     }
 }
 
-int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
-            hm_result* out) {
-    if (!ctx || !out || (!msg && len)) return HM_ERR_INVALID;
-    static const uint8_t empty_msg = 0;
-    if (!msg) msg = &empty_msg;
+int hm_scan_many(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
+    if (!ctx || n < 0 || (n > 0 && (!reqs || !outs))) return HM_ERR_INVALID;
+    for (int r = 0; r < n; ++r)
+        if (!reqs[r].msg && reqs[r].len) return HM_ERR_INVALID;
     std::lock_guard<std::mutex> g(ctx->mu);
     const auto t0 = std::chrono::steady_clock::now();
-    const MsgPlan mp = plan_message(msg, len);
-    const int n = (int)ctx->devs.size();
-    const bool empty = lo > hi;
-    // contiguous shards: span_m1 + 1 = n*q + (rr + 1); shards 0..rr get q+1
-    const uint64_t span_m1 = empty ? 0 : hi - lo;
-    const uint64_t q = span_m1 / (uint64_t)n, rr = span_m1 % (uint64_t)n;
-    uint64_t start = lo;
-    for (int i = 0; i < n; ++i) {
-        uint64_t a = 0, b = 0;
-        bool e = empty;
-        if (!empty) {
-            const uint64_t cnt_m1 = q - 1u + ((uint64_t)i <= rr ? 1u : 0u);  // modular
-            e = (q == 0 && (uint64_t)i > rr);
-            a = start;
-            b = start + cnt_m1;
-            if (!e) start = b + 1;
-        }
-        int rc = enqueue_device_scan(ctx, ctx->devs[i], mp, a, b, e);
+    std::vector<hm_result> res(n);
+    for (auto& dv : ctx->devs) {
+        dv.evnext = 0;
+        dv.launches.clear();
+    }
+    uint64_t total = 0;
+    for (int r = 0; r < n; ++r)
+        if (reqs[r].lo <= reqs[r].hi) total += reqs[r].hi - reqs[r].lo + 1;  // wraps for 2^64
+    for (int c = 0; c < n; c += kMaxBatch) {
+        const int m = std::min(kMaxBatch, n - c);
+        int rc = scan_chunk(ctx, reqs + c, m, res.data() + c);
         if (rc) return rc;
     }
-    hm_result res{~0ull, 0};
-    if (n > 1 && ctx->merge_rccl) {
-        int rc = rccl_merge(ctx);
-        if (rc) return rc;
-        Device& d0 = ctx->devs[0];
-        HIPCHK(hipSetDevice(d0.ordinal));
-        HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, sizeof(hm_result), hipMemcpyDeviceToHost,
-                              d0.stream[0]));
-        for (auto& dv : ctx->devs) {
-            HIPCHK(hipSetDevice(dv.ordinal));
-            HIPCHK(hipStreamSynchronize(dv.stream[0]));
-        }
-        res = *d0.host_out;
-    } else {
-        for (auto& dv : ctx->devs) {
-            HIPCHK(hipSetDevice(dv.ordinal));
-            HIPCHK(hipMemcpyAsync(dv.host_out, dv.result, sizeof(hm_result),
-                                  hipMemcpyDeviceToHost, dv.stream[0]));
-        }
-        for (auto& dv : ctx->devs) {
-            HIPCHK(hipSetDevice(dv.ordinal));
-            HIPCHK(hipStreamSynchronize(dv.stream[0]));
-            if (lex_less(dv.host_out->hash, dv.host_out->nonce, res.hash, res.nonce))
-                res = *dv.host_out;
-        }
-    }
+    const int ndev = (int)ctx->devs.size();
     // stats
     hm_stats st{};
-    st.ndev = n;
-    st.nonces = empty ? 0 : span_m1 + 1;  // wraps to 0 for the full 2^64 range
+    st.ndev = ndev;
+    st.nonces = total;
     // aggregate per kernel instantiation; the dominant one has the most nonces
     struct Agg { std::string name; double ms = 0; uint64_t nonces = 0; int launches = 0;
                  int kind = 0, grid = 0; uint32_t comp = 0; uint64_t big = 0; };
@@ -577,9 +621,17 @@ int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t h
                      .count();
     ctx->last = st;
     ctx->have_stats = true;
-    *out = res;
+    for (int r = 0; r < n; ++r) outs[r] = res[r];
     return HM_OK;
 }
+
+int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
+            hm_result* out) {
+    if (!ctx || !out || (!msg && len)) return HM_ERR_INVALID;
+    hm_request q{msg, len, lo, hi};
+    return hm_scan_many(ctx, &q, 1, out);
+}
+
 
 int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
     if (!ctx || !out || !ctx->have_stats) return HM_ERR_INVALID;

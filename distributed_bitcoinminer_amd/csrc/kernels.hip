@@ -418,12 +418,13 @@ __global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A)
 // Second reduce pass and init
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restrict__ cand,
-                                                         uint32_t n, uint64_t* best) {
+                                                         uint32_t n, uint32_t stride,
+                                                         uint64_t* best) {
     __shared__ uint64_t sk[kBlock / kWaveSize], sn[kBlock / kWaveSize];
     uint64_t k = ~0ull, nn = ~0ull;
     if (threadIdx.x == 0) { k = best[0]; nn = best[1]; }
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint64_t k2 = cand[2 * i], n2 = cand[2 * i + 1];
+        const uint64_t k2 = cand[2 * (size_t)i * stride], n2 = cand[2 * (size_t)i * stride + 1];
         if (k2 < k || (k2 == k && n2 < nn)) { k = k2; nn = n2; }
     }
     wave_min(k, nn);
@@ -528,8 +529,9 @@ hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipSt
     return hipGetLastError();
 }
 
-hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s) {
-    hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, best);
+hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
+                       uint32_t stride) {
+    hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, stride, best);
     return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ constexpr int kBlock = 256;            // 4 waves per workgroup
 constexpr int kRecWords = 32;          // tile record stride: state[8], W[16], pad
 constexpr uint32_t kMaxTilesPerLaunch = 1u << 20;
 constexpr uint32_t kMaxCandWaves = 32768;  // per-launch candidate slots (waves)
+constexpr int kMaxBatch = 64;              // requests per hm_scan_many chunk
 
 // Tile planner: one thread per tile.
 struct PlanArgs {
@@ -101,8 +102,10 @@ hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s);
 int chained_blocks_per_cu();
 // K+W table of the final block for loop values t in [0, 10^f).
 hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s);
-// Fold n (key, nonce) pairs plus *best into *best (lexicographic min).
-hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s);
+// Fold n (key, nonce) pairs (pair i at cand + 2*i*stride) plus *best into
+// *best (lexicographic min).
+hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
+                       uint32_t stride = 1);
 hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);
 // Occupancy-derived persistent grid (workgroups) for the tiled kernel.
 int tiled_blocks_per_cu(int W1, bool straddle, bool trailer);

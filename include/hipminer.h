@@ -111,7 +111,21 @@ int hm_open(const int *devices, int ndev, hm_ctx **out);
 int hm_scan(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi,
             hm_result *out);
 
-/* Stats of the last successful hm_scan on ctx. */
+/* One request of a batch: the same meaning as hm_scan's arguments. */
+typedef struct hm_request {
+    const uint8_t *msg; /* borrowed for the call; may be NULL when len == 0 */
+    size_t len;
+    uint64_t lo, hi;    /* inclusive */
+} hm_request;
+
+/* Batch form of hm_scan: outs[i] = hm_scan(reqs[i]) for i < n.  All requests'
+ * GPU work is enqueued before one host synchronisation (SURVEY §8(f) rank 4:
+ * the server's FIFO (cmu440/bitcoin/server/server.go:211-219, 318-324) hands a
+ * miner one small chunk at a time; a miner or a future GPU-side server can
+ * batch them here).  outs is written only when the call returns HM_OK. */
+int hm_scan_many(hm_ctx *ctx, const hm_request *reqs, int n, hm_result *outs);
+
+/* Stats of the last successful hm_scan / hm_scan_many on ctx. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
 
 int hm_set_option(hm_ctx *ctx, int opt, int64_t value);

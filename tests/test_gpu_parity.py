@@ -226,3 +226,39 @@ def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
             assert fast == slow, (L, d, key)
             assert _lib.host_hash(m, fast[1]) == fast[0]
     assert len(seen) >= 40, len(seen)
+
+
+def test_multi_device_context_sharding(oracle_mod):
+    """The in-process multi-device path (contiguous shards + merge of 16-B
+    results) with device 0 opened as 2 and 3 'devices' on this 1-GPU box."""
+    cases = [(b"bradfitz", 0, 9999), (b"bradfitz", 5, 5), (b"bradfitz", 5, 6), (b"x", 5, 4),
+             (b"jonny greenwood", 10**9 - 777_777, 10**9 + 123_456),
+             (b"bradfitz", MAX - 100_000, MAX)]
+    for devs in ([0, 0], [0, 0, 0]):
+        with _lib.Context(devs) as c:
+            for m, lo, hi in cases:
+                assert c.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (devs, m, lo, hi)
+            assert c.stats()["ndev"] == len(devs)
+
+
+def test_scan_many_batches(oracle_mod):
+    """hm_scan_many == per-request hm_scan, across batch chunks (> kMaxBatch =
+    64 requests), empty requests, streams and multi-device contexts."""
+    rng = random.Random(4242)
+    reqs = []
+    for i in range(150):
+        L = rng.randrange(0, 130)
+        m = bytes(rng.randrange(256) for _ in range(L))
+        k = rng.randrange(1, 20)
+        lo = max(0, 10**k - rng.randrange(0, 3000))
+        hi = lo + rng.randrange(-5, 6000)
+        reqs.append((m, lo, max(hi, 0) if i % 17 else lo - 1))  # some empty
+    exp = [oracle_mod.c_scan(m, lo, hi) for m, lo, hi in reqs]
+    for devs, streams in (([0], 1), ([0], 4), ([0, 0], 1)):
+        with _lib.Context(devs) as c:
+            c.set_option(_lib.HM_OPT_STREAMS, streams)
+            assert c.scan_many(reqs) == exp, (devs, streams)
+            assert c.scan_many([]) == []
+    with _lib.Context([0]) as c:
+        assert c.scan_many([(b"bradfitz", 0, 10**7), (b"bradfitz", 0, 9999)]) == \
+            [(356393768206, 7645578), (1419516646206828, 9898)]
