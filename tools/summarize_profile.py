@@ -16,10 +16,13 @@ import os
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
+merge_into = os.path.join(dst, "pmc_summary.json")
 # segment nonces of bradfitz [0, 2^32) by kernel (planner: d=9 and d=10 share W1=4)
 NONCES = {"hm_tiled_kernel<4, false, false>": 900_000_000 + (2**32 - 10**9),
           "hm_tiled_kernel<4, true, false>": 90_000_000,
-          "hm_tiled_kernel<3, false, false>": 9_990_000}
+          "hm_tiled_kernel<3, false, false>": 9_990_000,
+          # cfg3 (120-B message): d = 8, 9, 10 are chained
+          "hm_chained_kernel": 2**32 - 10**7}
 
 
 def per_dispatch(path):
@@ -58,6 +61,11 @@ for name, nonces in NONCES.items():
         "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024 / n_l,
     }
 os.makedirs(dst, exist_ok=True)
-with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+if os.path.exists(merge_into):  # keep kernels summarised from other runs
+    with open(merge_into) as f:
+        prev = json.load(f)
+    prev.update(out)
+    out = prev
+with open(merge_into, "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))
