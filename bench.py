@@ -54,17 +54,20 @@ WORKLOADS = {
 }
 
 
-def profiled_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py)."""
+def profiled(kernel: str):
+    """PMC summary of `kernel` from the newest committed profile
+    (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py):
+    HBM bytes per launch and the effective clock, with the file it came from."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
                        reverse=True):
         with open(path) as f:
             summ = json.load(f)
         if kernel in summ:
-            return summ[kernel]["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
+            k = summ[kernel]
+            return k["hbm_bytes_per_launch"], k["f_eff_ghz_largest_dispatch"], \
+                os.path.relpath(path, ROOT)
+    return None, None, None
 OPS_PER_COMPRESSION = 1552           # SURVEY Appendix C
 PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T INT32 lane-ops/s
 CPU_SAMPLE = 50_000_000              # nonces for the 1-thread CPU baseline (~12 s on the GPU box host)
@@ -171,7 +174,7 @@ def main():
         avg_ms = st["dom_kernel_ms"] / launches
         ops_per_launch = st["dom_nonces"] / launches * OPS_PER_COMPRESSION * C
         achieved = ops_per_launch / (avg_ms * 1e-3) / 1e12
-        traffic, traffic_src = profiled_traffic(st["dom_kernel"])
+        traffic, f_eff, traffic_src = profiled(st["dom_kernel"])
         line = {
             "metric": "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of INT32 VALU roofline",
             "value": round(value, 3),
@@ -194,6 +197,8 @@ def main():
                          "frac": round(achieved / PEAK_TOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
+                         "f_eff_ghz": f_eff,
+                         "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
                          "kernel": st["dom_kernel"],
                          "launches_per_step": launches,
                          "avg_launch_ms": round(avg_ms, 3),
