@@ -51,6 +51,9 @@ WORKLOADS = {
                           "[rank*2^32, (rank+1)*2^32), all-gather of 16-B candidates"),
     "cfg3": (None, "cfg3: 120-B msg (random.Random(440)), C=2 (1 host-midstate block + 2 tail "
                    "blocks), 2^32 nonces per GPU, all-gather of 16-B candidates"),
+    # strong scaling: the whole [0, 2^40) split over the N ranks
+    "cfg4": (b"bradfitz", "cfg4: msg 'bradfitz', [0, 2^40) split contiguously over N GPUs "
+                          "(strong scaling), all-gather of 16-B candidates"),
 }
 
 
@@ -127,7 +130,13 @@ def main():
             dist.init_process_group(backend, rank=rank, world_size=world)
 
     ctx = _lib.Context([gpu])
-    lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1
+    if args.workload == "cfg4":
+        from distributed_bitcoinminer_amd.parallel import shard_range
+        total_nonces = 1 << 40
+        lo, hi = shard_range(0, total_nonces - 1, world, rank)
+    else:
+        total_nonces = world * PER_GPU
+        lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1
     dev = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
     cdev = torch.device("cuda", gpu)
     cand = torch.empty(2, dtype=torch.int64, device=dev)
@@ -166,7 +175,7 @@ def main():
     assert _lib.host_hash(msg, res[1]) == res[0], res
 
     if rank == 0:
-        total = world * PER_GPU * args.steps
+        total = total_nonces * args.steps
         value = total / elapsed / 1e9
         C = st["dom_compressions"]
         # per launch: algorithmic ops / average launch duration of the dominant kernel
@@ -184,11 +193,11 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.workload == "cfg4" else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (fixed message, contiguous nonce ranges; no dataset)",
-            "config": {"workload": desc, "nonces_per_gpu": PER_GPU,
+            "config": {"workload": desc, "nonces_per_gpu": total_nonces // world,
                        "parallelism": f"dp{world} (nonce shards)",
                        "merge": "RCCL all-gather" if world > 1 and backend == "nccl" else backend},
             "result": {"hash": res[0], "nonce": res[1]},

@@ -262,3 +262,27 @@ def test_scan_many_batches(oracle_mod):
     with _lib.Context([0]) as c:
         assert c.scan_many([(b"bradfitz", 0, 10**7), (b"bradfitz", 0, 9999)]) == \
             [(356393768206, 7645578), (1419516646206828, 9898)]
+
+
+def test_chunked_tile_launches(ctx):
+    """A segment with > 2^20 tiles is split into several launches (config 4 at
+    d=13 does this).  bradfitz at d=12 has V=5 (10^5-nonce tiles): 1.2e11
+    nonces = 1.2 M tiles -> 2 launches.  Checked by shard invariance across the
+    launch boundary and the generic kernel on a window around it."""
+    from distributed_bitcoinminer_amd.parallel import merge
+    lo, hi = 10**11, 10**11 + 120_000_000_000
+    seg = _lib.debug_plan(b"bradfitz", lo, hi)[0]
+    assert seg["kind"] == _lib.HM_KIND_TILED and seg["V"] == 5
+    whole = ctx.scan(b"bradfitz", lo, hi)
+    assert ctx.stats()["dom_launches"] >= 2
+    boundary = (lo // 10**5 + (1 << 20)) * 10**5  # first nonce of the 2nd launch
+    parts = [ctx.scan(b"bradfitz", lo, boundary - 7), ctx.scan(b"bradfitz", boundary - 6, hi)]
+    assert merge(parts) == whole
+    w_lo, w_hi = boundary - 30_000_000, boundary + 30_000_000
+    fast = ctx.scan(b"bradfitz", w_lo, w_hi)
+    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+    try:
+        assert ctx.scan(b"bradfitz", w_lo, w_hi) == fast
+    finally:
+        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+    assert _lib.host_hash(b"bradfitz", whole[1]) == whole[0]
