@@ -229,12 +229,19 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
 
         for (uint32_t t1 = 0; t1 < 10; ++t1) {
             for (uint32_t t0 = 0; t0 < 10; ++t0) {
-                const uint64_t L = (uint64_t)(((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift;
                 uint32_t m[16];
 #pragma unroll
                 for (int k = 0; k < 16; ++k) m[k] = W[k];
-                m[W1 - 1] = STRADDLE ? X0 + (uint32_t)(L >> 32) : X0;
-                m[W1] = X1 + (uint32_t)L;
+                if constexpr (STRADDLE) {
+                    // last digit opens W[W1], the tens digit closes W[W1-1]:
+                    // work on W[W1-1] depends on t1 only and is hoisted out
+                    // of the t0 loop
+                    m[W1 - 1] = X0 + (0x30u + t1);
+                    m[W1] = X1 + ((0x30u + t0) << 24);
+                } else {
+                    m[W1 - 1] = X0;
+                    m[W1] = X1 + ((((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift);
+                }
                 constexpr uint32_t VM = (1u << (W1 - 1)) | (1u << W1);
                 State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
                 sha_rounds<VM>(s, m);
