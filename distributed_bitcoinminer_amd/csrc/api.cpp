@@ -489,7 +489,7 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
     return host_hash(msg ? msg : &empty, msg ? len : 0, nonce);
 }
 
-int hm_version(void) { return (1 << 16) | 0; }
+int hm_version(void) { return (1 << 16) | 1; }  // 1.1: hm_scan_many, hm_stats.dom_*
 
 const char* hm_strerror(int rc) {
     switch (rc) {

@@ -69,6 +69,48 @@ func (m *Miner) ScanInclusive(data string, lo, hi uint64) (hash, nonce uint64, e
 	return uint64(out.hash), uint64(out.nonce), nil
 }
 
+// Request is one (data, lo, hi) job of a batch; lo and hi are inclusive.
+type Request struct {
+	Data   string
+	Lo, Hi uint64
+}
+
+// ScanMany runs hm_scan_many: every request's GPU work is queued before one
+// synchronisation.  Results are in request order.
+func (m *Miner) ScanMany(reqs []Request) ([][2]uint64, error) {
+	if len(reqs) == 0 {
+		return nil, nil
+	}
+	// C memory for the request array: it holds pointers (to the message bytes),
+	// which the cgo rules do not allow in Go memory passed to C.
+	creqs := (*[1 << 20]C.hm_request)(C.malloc(C.size_t(len(reqs)) * C.size_t(unsafe.Sizeof(C.hm_request{}))))[:len(reqs):len(reqs)]
+	defer C.free(unsafe.Pointer(&creqs[0]))
+	cbufs := make([]unsafe.Pointer, 0, len(reqs))
+	defer func() {
+		for _, b := range cbufs {
+			C.free(b)
+		}
+	}()
+	for i, r := range reqs {
+		var p *C.uint8_t
+		if len(r.Data) > 0 {
+			b := C.CBytes([]byte(r.Data))
+			cbufs = append(cbufs, b)
+			p = (*C.uint8_t)(b)
+		}
+		creqs[i] = C.hm_request{msg: p, len: C.size_t(len(r.Data)), lo: C.uint64_t(r.Lo), hi: C.uint64_t(r.Hi)}
+	}
+	outs := make([]C.hm_result, len(reqs))
+	if rc := C.hm_scan_many(m.ctx, &creqs[0], C.int(len(reqs)), &outs[0]); rc != 0 {
+		return nil, Error{int(rc)}
+	}
+	res := make([][2]uint64, len(reqs))
+	for i, o := range outs {
+		res[i] = [2]uint64{uint64(o.hash), uint64(o.nonce)}
+	}
+	return res, nil
+}
+
 // EvalRequest is the drop-in for miner.go:63-76: it keeps the reference's
 // `upper := Upper + 1` uint64 wrap (Upper == MaxUint64 scans nothing) and
 // its initial (MaxUint64, 0).
