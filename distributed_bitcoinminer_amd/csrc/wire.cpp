@@ -310,7 +310,10 @@ std::string marshal_bitcoin(const BitcoinMsg& m) {
 bool unmarshal_bitcoin(const std::string& payload, BitcoinMsg* m) {
     *m = BitcoinMsg();
     std::map<std::string, JVal> o;
+    // Go's Unmarshal validates the whole input first: a syntax error decodes
+    // nothing; type errors on single fields leave just those fields zero.
     const bool ok = parse_object(payload, &o);
+    if (!ok) return false;
     auto u64 = [&](const char* k, uint64_t* dst) {
         auto it = o.find(k);
         if (it != o.end() && it->second.kind == JVal::NUM && it->second.int_ok && !it->second.neg)
@@ -326,7 +329,7 @@ bool unmarshal_bitcoin(const std::string& payload, BitcoinMsg* m) {
     u64("upper", &m->upper);
     u64("hash", &m->hash);
     u64("nonce", &m->nonce);
-    return ok;
+    return true;
 }
 
 }  // namespace wire

@@ -41,8 +41,9 @@ struct BitcoinMsg {
     uint64_t lower = 0, upper = 0, hash = 0, nonce = 0;
 };
 std::string marshal_bitcoin(const BitcoinMsg& m);       // json.Marshal
-// json.Unmarshal into a zero Message: fields with type errors stay zero; the
-// return value says whether the whole payload parsed (the miner ignores it).
+// json.Unmarshal into a zero Message: a syntax error leaves the whole Message
+// zero (Go validates before decoding), fields with type errors stay zero; the
+// return value says whether the payload was valid JSON (the miner ignores it).
 bool unmarshal_bitcoin(const std::string& payload, BitcoinMsg* m);
 
 // Parse one flat JSON object; keys are lower-cased.  Returns false on syntax

@@ -118,3 +118,19 @@ def test_client_detects_lost_server(tool):
     finally:
         if p.poll() is None:
             p.kill()
+
+
+def test_bitcoin_codec_go_error_semantics(tool):
+    # syntax error: Go decodes nothing (checkValid runs first)
+    assert run(tool, "bitcoin", '{"Type":1,"Data":"x","Lower":5') == \
+        '0 {"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}'
+    assert run(tool, "bitcoin", 'garbage') == \
+        '0 {"Type":0,"Data":"","Lower":0,"Upper":0,"Hash":0,"Nonce":0}'
+    # type error: the other fields still decode
+    assert run(tool, "bitcoin", '{"Data":"abc","Lower":5,"Upper":"x"}') == \
+        '1 {"Type":0,"Data":"abc","Lower":5,"Upper":0,"Hash":0,"Nonce":0}'
+    # the Python mirror agrees
+    m, err = bitcoin.unmarshal(b'{"Type":1,"Data":"x","Lower":5')
+    assert err is not None and m == bitcoin.Message()
+    m, err = bitcoin.unmarshal(b'{"Data":"abc","Lower":5,"Upper":"x"}')
+    assert err is not None and (m.Data, m.Lower, m.Upper) == (b"abc", 5, 0)
