@@ -119,7 +119,10 @@ def main():
 
     gpu = local_rank if backend == "nccl" else 0
     dist = None
-    if world > 1:
+    # HM_BENCH_FORCE_DIST=1 runs the distributed path even at world size 1
+    # (rehearses the RCCL all-gather on a 1-GPU box).
+    use_dist = world > 1 or os.environ.get("HM_BENCH_FORCE_DIST") == "1"
+    if use_dist:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(gpu)
@@ -144,7 +147,7 @@ def main():
 
     def step():
         local = ctx.scan(msg, lo, hi)
-        if world == 1:
+        if dist is None:
             return local
         cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
         dist.all_gather_into_tensor(gathered, cand)  # 16 B per rank over RCCL
@@ -199,7 +202,8 @@ def main():
             "data": "synthetic (fixed message, contiguous nonce ranges; no dataset)",
             "config": {"workload": desc, "nonces_per_gpu": total_nonces // world,
                        "parallelism": f"dp{world} (nonce shards)",
-                       "merge": "RCCL all-gather" if world > 1 and backend == "nccl" else backend},
+                       "merge": ("RCCL all-gather" if backend == "nccl" else backend)
+                                if dist is not None else "none (1 rank)"},
             "result": {"hash": res[0], "nonce": res[1]},
             "roofline": {"bound": "valu", "achieved": round(achieved, 3),
                          "peak": round(PEAK_TOPS, 3), "unit": "T int32 lane-ops/s",
