@@ -97,3 +97,44 @@ def test_three_miners_under_server_model(oracle_mod):
                 p.wait(timeout=60)
             except subprocess.TimeoutExpired:
                 p.kill()
+
+
+def test_config5_eight_miners_near_max(oracle_mod):
+    """Config 5 shape: 8 GPU miner processes, the four SURVEY messages as queued
+    client requests near 2^64-1 (20-digit nonces).  Each request is split as
+    server.go:165-205 splits it; the merged answer must equal the A-inv-7
+    model computed with direct scans of the same chunks."""
+    import random
+    from distributed_bitcoinminer_amd import _lib, miner
+    rng = random.Random(440)
+    long120 = bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
+    msgs = [b"bradfitz", b"thom yorke", long120, b"jonny greenwood"]
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=100)
+    procs = [_spawn(srv) for _ in range(8)]
+    try:
+        cids = [srv.accept(timeout=180) for _ in procs]
+        for c in cids:
+            assert srv.read(c, timeout=120) == bitcoin.marshal(bitcoin.NewJoin())
+        with _lib.Context([0]) as ctx:
+            direct = miner.Miner(ctx=ctx)
+            for data in msgs:                 # FIFO: one client request at a time
+                lo, up = MAX - 1 - (1 << 30), MAX - 1
+                chunks = sm.load_balance(lo, up, len(cids))
+                assert len(chunks) == 8 and chunks[-1][1] == MAX
+                for c, (a, b) in zip(cids, chunks):
+                    srv.write(c, bitcoin.marshal(bitcoin.NewRequest(data, a, b)))
+                got = []
+                for c in cids:
+                    r, _ = bitcoin.unmarshal(srv.read(c, timeout=300))
+                    got.append((r.Hash, r.Nonce))
+                assert got[-1] == (MAX, 0)        # the chunk ending at 2^64-1 scans nothing
+                exp = sm.expected_client_result(data, lo, up, 8, direct.scan)
+                assert sm.merge_in_arrival_order(got) == exp
+                assert _lib.host_hash(data, exp[1]) == exp[0]
+    finally:
+        srv.close()
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()
