@@ -33,6 +33,8 @@
  *
  * Threading: calls on one context are serialised by an internal mutex; every
  * call re-binds its device (hipSetDevice), so Go may call from any OS thread.
+ * hm_close must not race other calls on the same context (the caller owns
+ * the context's lifetime, as with any C handle).
  *
  * Errors: 0 = HM_OK; negative codes below; hm_strerror() describes them.
  * Nothing aborts the process and there is no CPU fallback: a failed GPU scan
