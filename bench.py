@@ -136,7 +136,7 @@ def main():
     if args.workload == "cfg4":
         from distributed_bitcoinminer_amd.parallel import shard_range
         total_nonces = 1 << 40
-        lo, hi = shard_range(0, total_nonces - 1, world, rank)
+        lo, hi = shard_range(0, total_nonces - 1, world, rank, msg=msg)  # cost-weighted
     else:
         total_nonces = world * PER_GPU
         lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1

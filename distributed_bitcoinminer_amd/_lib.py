@@ -98,6 +98,9 @@ def load() -> ctypes.CDLL:
         lib.hm_close.argtypes = [ctypes.c_void_p]
         lib.hm_version.restype = ctypes.c_int
         lib.hm_version.argtypes = []
+        lib.hm_partition.restype = ctypes.c_int
+        lib.hm_partition.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
         lib.hm_debug_plan.restype = ctypes.c_int
         lib.hm_debug_plan.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -195,15 +198,30 @@ def host_hash(msg, nonce: int) -> int:
     return int(load().hm_hash(m, len(m), nonce))
 
 
+def partition(msg, lo: int, hi: int, n: int) -> list:
+    """hm_partition: n contiguous shards of [lo, hi] with near-equal modelled
+    GPU cost for msg; each entry is (lo_i, hi_i) or None when empty.  Host-only."""
+    m = as_bytes(msg)
+    buf = (ctypes.c_uint64 * (2 * max(1, n)))()
+    rc = load().hm_partition(m, len(m), lo, hi, n, buf)
+    if rc != HM_OK:
+        raise HipMinerError(rc, "hm_partition")
+    out = []
+    for i in range(n):
+        a, b = int(buf[2 * i]), int(buf[2 * i + 1])
+        out.append((a, b) if a <= b else None)
+    return out
+
+
 def debug_plan(msg, lo: int, hi: int, force_generic: bool = False) -> list[dict]:
     m = as_bytes(msg)
     cap = 32
-    buf = (ctypes.c_int64 * (8 * cap))()
+    buf = (ctypes.c_int64 * (9 * cap))()
     n = load().hm_debug_plan(m, len(m), lo, hi, int(force_generic), buf, cap)
-    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle")
+    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost")
     out = []
     for i in range(min(n, cap)):
-        row = dict(zip(keys, buf[8 * i: 8 * i + 8]))
+        row = dict(zip(keys, buf[9 * i: 9 * i + 9]))
         row["lo"] &= (1 << 64) - 1
         row["hi"] &= (1 << 64) - 1
         out.append(row)

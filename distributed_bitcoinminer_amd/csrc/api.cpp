@@ -428,22 +428,15 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
     for (int r = 0; r < nreq; ++r) {
         const hm_request& q = reqs[r];
         plans[r] = plan_message(q.msg ? q.msg : &empty_msg, q.msg ? q.len : 0);
-        const bool empty = q.lo > q.hi;
-        // contiguous shards: span_m1 + 1 = ndev*qq + (rr + 1); shards 0..rr get qq+1
-        const uint64_t span_m1 = empty ? 0 : q.hi - q.lo;
-        const uint64_t qq = span_m1 / (uint64_t)ndev, rr = span_m1 % (uint64_t)ndev;
-        uint64_t start = q.lo;
+        // contiguous shards of equal modelled cost
+        const std::vector<Shard> sh =
+            partition_range(plans[r], q.lo, q.hi, ndev, ctx->force_generic);
         for (int i = 0; i < ndev; ++i) {
             DevReq& dr = per_dev[i][r];
             dr.mp = &plans[r];
-            dr.empty = empty || (qq == 0 && (uint64_t)i > rr);
-            dr.lo = dr.hi = 0;
-            if (!dr.empty) {
-                const uint64_t cnt_m1 = qq - 1u + ((uint64_t)i <= rr ? 1u : 0u);  // modular
-                dr.lo = start;
-                dr.hi = start + cnt_m1;
-                start = dr.hi + 1;
-            }
+            dr.empty = sh[i].empty;
+            dr.lo = sh[i].empty ? 0 : sh[i].lo;
+            dr.hi = sh[i].empty ? 0 : sh[i].hi;
         }
     }
     for (int i = 0; i < ndev; ++i) {
@@ -489,7 +482,20 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
     return host_hash(msg ? msg : &empty, msg ? len : 0, nonce);
 }
 
-int hm_version(void) { return (1 << 16) | 1; }  // 1.1: hm_scan_many, hm_stats.dom_*
+int hm_version(void) { return (1 << 16) | 2; }  // 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition
+
+int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
+                 uint64_t* bounds) {
+    if (n <= 0 || !bounds || (len > 0 && !msg)) return HM_ERR_INVALID;
+    static const uint8_t empty = 0;
+    const MsgPlan mp = plan_message(msg ? msg : &empty, msg ? len : 0);
+    const std::vector<Shard> sh = partition_range(mp, lo, hi, n, false);
+    for (int i = 0; i < n; ++i) {
+        bounds[2 * i] = sh[i].empty ? 1 : sh[i].lo;
+        bounds[2 * i + 1] = sh[i].empty ? 0 : sh[i].hi;
+    }
+    return HM_OK;
+}
 
 const char* hm_strerror(int rc) {
     switch (rc) {
@@ -640,8 +646,8 @@ int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
 }
 
 // ---- debug exports for host-side tests (not part of include/hipminer.h) ----
-// Writes up to `cap` segment descriptors as 8 x int64:
-//   d, lo, hi, kind, W1, V, trailer, straddle
+// Writes up to `cap` segment descriptors as 9 x int64:
+//   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (model cycles / 64 nonces)
 int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
                   int64_t* outv, int cap) {
     if (lo > hi) return 0;
@@ -651,9 +657,10 @@ int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int 
     int i = 0;
     for (; i < (int)segs.size() && i < cap; ++i) {
         const SegPlan& s = segs[i];
-        int64_t* o = outv + 8 * i;
+        int64_t* o = outv + 9 * i;
         o[0] = s.d; o[1] = (int64_t)s.lo; o[2] = (int64_t)s.hi; o[3] = s.kind;
         o[4] = s.W1; o[5] = s.V; o[6] = s.trailer; o[7] = s.straddle;
+        o[8] = (int64_t)seg_cost(s);
     }
     return (int)segs.size();
 }

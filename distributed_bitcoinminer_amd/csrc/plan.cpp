@@ -1,6 +1,7 @@
 // plan.cpp -- host planner (see plan.hpp and DESIGN.md §3).
 #include "plan.hpp"
 
+#include <math.h>
 #include <string.h>
 
 #include <algorithm>
@@ -115,6 +116,64 @@ std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, boo
         if (s.lo > s.hi) continue;
         layout(mp, s, force_generic);
         out.push_back(s);
+    }
+    return out;
+}
+
+double seg_cost(const SegPlan& s) {
+    // tiled, one block: model cycles by W1 (straddle variants differ by < 1 %)
+    static const double kTiled[14] = {0,    5018, 4972, 4877, 4785, 4691, 4596,
+                                      4502, 4408, 4505, 4541, 4447, 4352, 4258};
+    switch (s.kind) {
+        case HM_KIND_TILED:
+            if (s.trailer) return 7780.0;  // digit block + constant trailer block
+            return kTiled[std::min(std::max(s.W1, 1), 13)];
+        case HM_KIND_CHAINED:
+            return 3481.0;  // per-lane block 0; table-driven final block
+        default:
+            // generic: every tail block per lane, no hoisting (estimate)
+            return 6000.0 * s.nb;
+    }
+}
+
+std::vector<Shard> partition_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, int n,
+                                   bool force_generic) {
+    std::vector<Shard> out(n > 0 ? n : 0, Shard{0, 0, true});
+    if (n <= 0 || lo > hi) return out;
+    typedef unsigned __int128 u128;
+    const std::vector<SegPlan> segs = plan_range(mp, lo, hi, force_generic);
+    std::vector<long double> cost(segs.size());
+    long double total = 0;
+    for (size_t i = 0; i < segs.size(); ++i) {
+        cost[i] = (long double)(segs[i].hi - segs[i].lo + 1) * seg_cost(segs[i]);
+        total += cost[i];
+    }
+    // start[i] = offset of shard i's first nonce from lo; start[n] = count
+    const u128 count = (u128)(hi - lo) + 1;
+    std::vector<u128> start(n + 1);
+    start[0] = 0;
+    start[n] = count;
+    size_t si = 0;
+    long double before = 0;  // cost of the segments ahead of segs[si]
+    for (int i = 1; i < n; ++i) {
+        const long double target = total * i / n;
+        while (si < segs.size() && before + cost[si] <= target) before += cost[si++];
+        u128 b = count;
+        if (si < segs.size()) {
+            const uint64_t cnt_m1 = segs[si].hi - segs[si].lo;
+            long double k = floorl((target - before) / seg_cost(segs[si]));
+            if (k < 0) k = 0;
+            const u128 kk = k > (long double)cnt_m1 ? (u128)cnt_m1 + 1 : (u128)(uint64_t)k;
+            b = (u128)(segs[si].lo - lo) + kk;
+        }
+        start[i] = std::min(count, std::max(b, start[i - 1]));
+    }
+    for (int i = 0; i < n; ++i) {
+        if (start[i + 1] > start[i]) {
+            out[i].empty = false;
+            out[i].lo = lo + (uint64_t)start[i];
+            out[i].hi = lo + (uint64_t)(start[i + 1] - 1);
+        }
     }
     return out;
 }

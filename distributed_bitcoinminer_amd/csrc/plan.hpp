@@ -46,6 +46,22 @@ uint64_t pow10_u64(uint32_t k);  // k <= 19
 MsgPlan plan_message(const uint8_t* msg, uint64_t len);
 // Segment list for inclusive [lo, hi] (lo <= hi).
 std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic);
+// Modelled GPU cost of one nonce of segment s: SIMD cycles per 64 nonces of
+// the kernel instantiation that runs it, from the issue model of DESIGN.md §4
+// (half-rate 4.28, full-rate 3.45 cycles) applied to the ISA audit
+// (profiles/r01/isa_audit.txt).  Only shard balancing uses it.
+double seg_cost(const SegPlan& s);
+
+struct Shard {
+    uint64_t lo, hi;  // inclusive; meaningful only when !empty
+    bool empty;
+};
+// Split inclusive [lo, hi] into n contiguous, ascending shards of near-equal
+// modelled cost (sum over nonces of seg_cost), SURVEY §8(e).  Shards cover
+// [lo, hi] exactly; a shard is empty when the range has too few nonces.
+// lo > hi gives n empty shards.
+std::vector<Shard> partition_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, int n,
+                                   bool force_generic);
 // Host SHA-256 of msg ‖ ' ' ‖ decimal(nonce), first 8 bytes big-endian.
 uint64_t host_hash(const uint8_t* msg, uint64_t len, uint64_t nonce);
 // K[i] + W[i] of the constant trailer block of a trailer segment.

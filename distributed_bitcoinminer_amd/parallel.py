@@ -18,11 +18,17 @@ import numpy as np
 MAXU64 = (1 << 64) - 1
 
 
-def shard_range(lo: int, hi: int, world: int, rank: int):
+def shard_range(lo: int, hi: int, world: int, rank: int, msg=None):
     """Contiguous shard `rank` of inclusive [lo, hi]; None when empty.
 
-    count = hi-lo+1 = world*q + (rr+1): shards 0..rr get q+1 nonces, the rest q
-    (the same split hm_scan uses across the devices of one context)."""
+    With ``msg``: the cost-weighted split of hm_partition (the one hm_scan uses
+    across the devices of one context): digit segments whose kernel costs more
+    per nonce get fewer nonces, so ranks finish together.
+    Without: equal counts, count = hi-lo+1 = world*q + (rr+1), shards 0..rr
+    get q+1 nonces, the rest q."""
+    if msg is not None:
+        from . import _lib
+        return _lib.partition(msg, lo, hi, world)[rank]
     if lo > hi:
         return None
     span_m1 = hi - lo
@@ -58,7 +64,7 @@ def distributed_scan(msg, lo: int, hi: int, scan_fn: Callable, device=None):
     import torch.distributed as dist
 
     rank, world = dist.get_rank(), dist.get_world_size()
-    shard = shard_range(lo, hi, world, rank)
+    shard = shard_range(lo, hi, world, rank, msg=msg)
     local = scan_fn(msg, shard[0], shard[1]) if shard is not None else (MAXU64, 0)
     t = torch.from_numpy(_pack(local))
     if device is not None:

@@ -138,3 +138,27 @@ func Hash(msg string, nonce uint64) uint64 {
 	}
 	return uint64(C.hm_hash(p, C.size_t(len(msg)), C.uint64_t(nonce)))
 }
+
+// Partition splits the inclusive range [lo, hi] into n contiguous shards of
+// near-equal modelled GPU cost for data (hm_partition; host-only).  Shard i
+// is [out[i][0], out[i][1]]; an empty shard has out[i][0] > out[i][1].  A
+// process-per-GPU launcher gives shard i to the miner on GPU i.
+func Partition(data string, lo, hi uint64, n int) ([][2]uint64, error) {
+	if n <= 0 {
+		return nil, Error{int(C.HM_ERR_INVALID)}
+	}
+	var p *C.uint8_t
+	if len(data) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
+	}
+	bounds := make([]C.uint64_t, 2*n)
+	if rc := C.hm_partition(p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi),
+		C.int(n), &bounds[0]); rc != C.HM_OK {
+		return nil, Error{int(rc)}
+	}
+	out := make([][2]uint64, n)
+	for i := range out {
+		out[i] = [2]uint64{uint64(bounds[2*i]), uint64(bounds[2*i+1])}
+	}
+	return out, nil
+}

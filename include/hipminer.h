@@ -109,7 +109,8 @@ int hm_open(const int *devices, int ndev, hm_ctx **out);
 
 /* Min-hash scan of the inclusive range [lo, hi] (see semantics above).  With
  * several devices the range is sharded contiguously and the per-device 16-B
- * candidates are merged (RCCL all-gather when HM_OPT_MERGE_RCCL is set). */
+ * candidates are merged (RCCL all-gather when HM_OPT_MERGE_RCCL is set); the
+ * shards are those of hm_partition (cost-weighted). */
 int hm_scan(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi,
             hm_result *out);
 
@@ -126,6 +127,18 @@ typedef struct hm_request {
  * miner one small chunk at a time; a miner or a future GPU-side server can
  * batch them here).  outs is written only when the call returns HM_OK. */
 int hm_scan_many(hm_ctx *ctx, const hm_request *reqs, int n, hm_result *outs);
+
+/* Split the inclusive range [lo, hi] into n contiguous, ascending shards of
+ * near-equal modelled GPU cost for msg (digit segments whose kernels cost more
+ * per nonce get fewer nonces).  bounds[2i], bounds[2i+1] = shard
+ * i's inclusive [lo, hi]; an empty shard is written as [1, 0].  The shards
+ * cover [lo, hi] exactly, so per-shard hm_scan results merged by (hash, nonce)
+ * minimum equal hm_scan over [lo, hi].  Host-only; needs no GPU.  This is how
+ * hm_scan shards one request across a multi-device context, and what a
+ * process-per-GPU caller (torch.distributed ranks, one Go miner per GPU) uses
+ * to cut its range. */
+int hm_partition(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int n,
+                 uint64_t *bounds);
 
 /* Stats of the last successful hm_scan / hm_scan_many on ctx. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);

@@ -229,10 +229,13 @@ def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
 
 
 def test_multi_device_context_sharding(oracle_mod):
-    """The in-process multi-device path (contiguous shards + merge of 16-B
-    results) with device 0 opened as 2 and 3 'devices' on this 1-GPU box."""
+    """The in-process multi-device path (cost-weighted contiguous shards of
+    hm_partition + merge of 16-B results) with device 0 opened as 2 and 3
+    'devices' on this 1-GPU box.  The m=45 case crosses 9 -> 10 digits, where
+    the trailer block doubles the per-nonce cost, so its shards are uneven."""
     cases = [(b"bradfitz", 0, 9999), (b"bradfitz", 5, 5), (b"bradfitz", 5, 6), (b"x", 5, 4),
              (b"jonny greenwood", 10**9 - 777_777, 10**9 + 123_456),
+             (b"a" * 45, 10**9 - 900_000, 10**9 + 300_000),
              (b"bradfitz", MAX - 100_000, MAX)]
     for devs in ([0, 0], [0, 0, 0]):
         with _lib.Context(devs) as c:
