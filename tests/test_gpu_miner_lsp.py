@@ -138,3 +138,66 @@ def test_config5_eight_miners_near_max(oracle_mod):
                 p.wait(timeout=60)
             except subprocess.TimeoutExpired:
                 p.kill()
+
+
+def test_server_sim_reassigns_a_killed_miner(oracle_mod):
+    """The server's whole event loop (ServerSim, server.go:207-400) over the
+    fake LSP transport with 3 GPU miner processes.  One miner is killed before
+    its chunk arrives: the LSP layer reports it lost after EpochLimit silent
+    epochs (-> the server's drop path, :326-376), its chunk is re-sent to a
+    surviving miner, and the client's Result equals the A-inv-7 model."""
+    import signal
+    import time
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=20)
+    procs = [_spawn(srv) for _ in range(3)]
+    client = 10_000                       # the client's conn id (not an LSP peer here)
+    data, lo, up = b"jonny greenwood", 10**9, 10**9 + 30_000_000
+    try:
+        cids = [srv.accept(timeout=180) for _ in procs]
+        sim = sm.ServerSim()
+        for c in cids:
+            assert srv.read(c, timeout=120) == bitcoin.marshal(bitcoin.NewJoin())
+            assert sim.miner_join(c) == []
+        # accept order need not follow spawn order, so the killed miner's conn
+        # is identified by its loss, not assumed
+        procs[1].send_signal(signal.SIGKILL)
+        procs[1].wait(timeout=30)
+        pending = list(sim.client_request(client, data, lo, up))
+        answers, final, dropped = [], None, set()
+        deadline = time.monotonic() + 240
+        while final is None and time.monotonic() < deadline:
+            for c, msg in pending:
+                if c == client:
+                    final = (msg.Hash, msg.Nonce)
+                else:
+                    srv.write(c, bitcoin.marshal(msg))
+            pending = []
+            for c in cids:
+                if c in dropped:
+                    continue
+                if srv.is_lost(c):
+                    dropped.add(c)
+                    pending += sim.drop(c)
+                    continue
+                try:
+                    raw = srv.by_id[c].ready.get(timeout=0.05)
+                except Exception:
+                    continue
+                res, err = bitcoin.unmarshal(raw)
+                assert err is None and res.Type == bitcoin.Result
+                answers.append((c, (res.Hash, res.Nonce)))
+                pending += sim.miner_result(c, res.Hash, res.Nonce)
+        assert final is not None, "no Result within the deadline"
+        assert len(dropped) == 1              # exactly the killed miner
+        assert len(answers) == 3              # two own chunks + the reassigned one
+        assert final == sm.merge_in_arrival_order([r for _, r in answers])
+        exp = sm.expected_client_result(data, lo, up, 3,
+                                        lambda d, a, b: oracle_mod.c_miner_eval(d, a, b))
+        assert final == exp
+    finally:
+        srv.close()
+        for p in procs:
+            try:
+                p.wait(timeout=60)
+            except subprocess.TimeoutExpired:
+                p.kill()

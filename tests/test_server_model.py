@@ -32,3 +32,160 @@ def test_expected_client_result_config1(oracle_mod):
     assert chunks[-1][1] == MAX
     res = sm.expected_client_result(b"bradfitz", lo, MAX - 1, 3, miner_scan)
     assert res == oracle_mod.c_scan(b"bradfitz", lo, chunks[-1][0], threads=4)
+
+
+# ---- ServerSim: the server's event loop (server.go:207-400) -----------------
+
+def _reqs(writes):
+    """Requests among the writes: {miner_id: (data, lower, upper)}."""
+    from distributed_bitcoinminer_amd import bitcoin
+    return {c: (m.Data, m.Lower, m.Upper) for c, m in writes if m.Type == bitcoin.Request}
+
+
+def _results(writes):
+    from distributed_bitcoinminer_amd import bitcoin
+    return [(c, (m.Hash, m.Nonce)) for c, m in writes if m.Type == bitcoin.Result]
+
+
+class _Fleet:
+    """Miners that answer with the CPU oracle's miner_eval (miner.go:63-76)."""
+
+    def __init__(self, oracle_mod):
+        self.o = oracle_mod
+        self.jobs = {}
+
+    def got(self, writes):
+        for c, job in _reqs(writes).items():
+            self.jobs.setdefault(c, []).append(job)
+
+    def answer(self, sim, mid):
+        data, lo, up = self.jobs[mid].pop(0)
+        h, n = self.o.c_miner_eval(data, lo, up, threads=2)
+        w = sim.miner_result(mid, h, n)
+        self.got(w)
+        return w, (h, n)
+
+
+def _scan(oracle_mod):
+    return lambda d, a, b: oracle_mod.c_miner_eval(d, a, b, threads=2)
+
+
+def test_sim_no_failures_matches_model(oracle_mod):
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    for mid in (11, 12, 13):
+        assert sim.miner_join(mid) == []
+    w = sim.client_request(1, b"bradfitz", 0, 9999)
+    fleet.got(w)
+    assert [(c, r[1], r[2]) for c, r in _reqs(w).items()] == \
+        [(11, 0, 3334), (12, 3334, 6667), (13, 6667, 10000)]
+    arrivals = []
+    for mid in (13, 11, 12):
+        w, r = fleet.answer(sim, mid)
+        arrivals.append(r)
+    assert _results(w) == [(1, sm.merge_in_arrival_order(arrivals))]
+    assert _results(w)[0][1] == sm.expected_client_result(
+        b"bradfitz", 0, 9999, 3, _scan(oracle_mod), order=[2, 0, 1])
+
+
+def test_sim_miner_drop_waits_for_next_result(oracle_mod):
+    """No idle miner: the dropped chunk queues until a miner answers (:285-304)."""
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    for mid in (1, 2, 3):
+        sim.miner_join(mid)
+    fleet.got(sim.client_request(9, b"thom yorke", 1000, 40000))
+    lost = fleet.jobs.pop(2)[0]
+    assert sim.drop(2) == [] and len(sim.dropped) == 1
+    w, r1 = fleet.answer(sim, 1)
+    assert _reqs(w) == {1: lost}                      # miner 1 inherits miner 2's chunk
+    w, r3 = fleet.answer(sim, 3)
+    assert _results(w) == []
+    w, r2 = fleet.answer(sim, 1)
+    expect = sm.merge_in_arrival_order([r1, r3, r2])
+    assert _results(w) == [(9, expect)]
+    assert expect == sm.expected_client_result(b"thom yorke", 1000, 40000, 3, _scan(oracle_mod))
+
+
+def test_sim_miner_drop_goes_to_idle_miner(oracle_mod):
+    """More miners than nonces leaves idle miners; a drop is reassigned at once (:339-369)."""
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    for mid in range(1, 6):
+        sim.miner_join(mid)
+    w = sim.client_request(7, b"bradfitz", 0, 1)
+    fleet.got(w)
+    assert sorted(_reqs(w)) == [1, 2]                 # totalLoad = 2 chunks of 1
+    lost = fleet.jobs.pop(2)[0]
+    w = sim.drop(2)
+    assert _reqs(w) == {3: lost}                      # first idle miner in join order
+    fleet.got(w)
+    fleet.answer(sim, 3)
+    w, _ = fleet.answer(sim, 1)
+    assert _results(w)[0][1] == sm.expected_client_result(b"bradfitz", 0, 1, 5, _scan(oracle_mod),
+                                                          order=[1, 0])
+
+
+def test_sim_join_takes_queued_chunk(oracle_mod):
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    sim.miner_join(1)
+    sim.miner_join(2)
+    fleet.got(sim.client_request(5, b"jonny greenwood", 200, 71010))
+    lost = fleet.jobs.pop(1)[0]
+    sim.drop(1)
+    w = sim.miner_join(3)
+    assert _reqs(w) == {3: lost} and sim.dropped == []
+    fleet.got(w)
+    fleet.answer(sim, 3)
+    w, _ = fleet.answer(sim, 2)
+    assert _results(w) == [(5, (1432633377981652, 56054))]   # SURVEY appendix B
+
+
+def test_sim_fifo_and_request_before_miners(oracle_mod):
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    assert sim.client_request(1, b"bradfitz", 0, 9999) == []
+    assert sim.client_request(2, b"bradfitz", 0, 99) == []
+    w = sim.miner_join(10)                              # :246-253
+    fleet.got(w)
+    assert _reqs(w) == {10: (b"bradfitz", 0, 10000)}
+    w, _ = fleet.answer(sim, 10)
+    assert _results(w) == [(1, (1419516646206828, 9898))]
+    assert _reqs(w) == {10: (b"bradfitz", 0, 100)}      # the next request starts at once
+    w, r = fleet.answer(sim, 10)
+    assert _results(w) == [(2, r)]
+
+
+def test_sim_client_drop(oracle_mod):
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    sim.miner_join(1)
+    sim.miner_join(2)
+    fleet.got(sim.client_request(5, b"bradfitz", 0, 999))
+    sim.client_request(6, b"bradfitz", 0, 9)
+    sim.client_request(8, b"x", 0, 9)
+    sim.drop(8)                                         # a waiting client: request removed
+    assert [j.conn_id for j in sim.waiting] == [6]
+    sim.drop(5)                                         # the current client
+    fleet.answer(sim, 1)
+    w, _ = fleet.answer(sim, 2)
+    assert _results(w) == []                            # no Result for a dropped client
+    assert _reqs(w) == {1: (b"bradfitz", 0, 5), 2: (b"bradfitz", 5, 10)}
+
+
+def test_sim_client_drop_after_miner_drop_stalls(oracle_mod):
+    """Dropping the client clears the queued chunk of a dropped miner, so the
+    request can never complete and later requests wait forever (:389-390)."""
+    sim, fleet = sm.ServerSim(), _Fleet(oracle_mod)
+    sim.miner_join(1)
+    sim.miner_join(2)
+    fleet.got(sim.client_request(5, b"bradfitz", 0, 999))
+    sim.drop(2)
+    sim.drop(5)
+    sim.client_request(6, b"bradfitz", 0, 9)
+    w, _ = fleet.answer(sim, 1)
+    assert w == [] and sim.curr is not None and [j.conn_id for j in sim.waiting] == [6]
+
+
+def test_sim_results_from_unknown_miners_are_ignored(oracle_mod):
+    sim = sm.ServerSim()
+    assert sim.miner_result(3, 1, 1) == []              # no current request
+    sim.miner_join(1)
+    sim.client_request(5, b"bradfitz", 0, 9)
+    assert sim.miner_result(99, 0, 0) == []             # not responsible
+    assert sim.curr.responses == 0 and sim.curr.min_hash == MAX
