@@ -10,6 +10,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 
 #include "wire.hpp"
@@ -178,6 +179,7 @@ LspClient::~LspClient() {
 
 void LspClient::send_raw(const std::string& bytes) {
     (void)!::send(fd_, bytes.data(), bytes.size(), 0);
+    last_tx_ = Clock::now();
 }
 
 // Move backlog into the window: every seq below (lowest unacked + WindowSize).
@@ -234,23 +236,35 @@ void LspClient::loop() {
     hb.type = lsp::kAck;
     hb.conn_id = conn_id_;
     const std::string heartbeat = lsp::encode(hb);
-    auto next_epoch = Clock::now() + std::chrono::milliseconds(p_.epoch_millis);
-    bool heard = false;
-    int silent = 0;
+    const auto epoch = std::chrono::milliseconds(p_.epoch_millis);
+    // Liveness follows the reference's timers (lsp/client_impl.go:257-286,
+    // server_impl.go:397-420): the peer is lost after EpochLimit epochs with
+    // nothing received.  The reference server resets its timers on every
+    // message, ACK(0) included, and sends its own reminder only after a
+    // silent epoch.  So this side keeps quiet for 1.5 epochs before its
+    // keepalive: the server's reminder fires first and each side keeps
+    // hearing the other while idle.  A client that beats every epoch would
+    // keep the server silent and then declare it lost.  With EpochLimit 1 the
+    // server must hear from us every epoch, hence half an epoch.
+    const auto keepalive = p_.epoch_limit >= 2 ? epoch * 3 / 2 : epoch / 2;
+    const auto drop_after = epoch * p_.epoch_limit;
+    auto last_rx = Clock::now();
+    auto next_tick = last_rx + epoch;  // data resend schedule
     for (;;) {
+        Clock::time_point wake;
         {
             std::lock_guard<std::mutex> g(mu_);
             if (stop_) return;
+            wake = std::min({next_tick, last_tx_ + keepalive, last_rx + drop_after});
         }
-        const int ms = std::max<int>(0, (int)std::chrono::duration_cast<std::chrono::milliseconds>(
-                                            next_epoch - Clock::now()).count());
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(wake - Clock::now());
         pollfd pf{fd_, POLLIN, 0};
-        const int pr = poll(&pf, 1, std::min(ms, 50));
+        const int pr = poll(&pf, 1, (int)std::max<int64_t>(0, std::min<int64_t>(ms.count() + 1, 50)));
         if (pr > 0) {
             const ssize_t n = recv(fd_, buf, sizeof buf, 0);
             lsp::Msg m;
             if (n > 0 && lsp::decode(std::string(buf, (size_t)n), &m) && lsp::intact(&m)) {
-                heard = true;
+                last_rx = Clock::now();
                 std::lock_guard<std::mutex> g(mu_);
                 if (m.type == lsp::kData) {
                     lsp::Msg ack;
@@ -279,28 +293,28 @@ void LspClient::loop() {
                 }
             }
         }
-        if (Clock::now() < next_epoch) continue;
-        next_epoch += std::chrono::milliseconds(p_.epoch_millis);
+        const auto now = Clock::now();
         std::lock_guard<std::mutex> g(mu_);
-        silent = heard ? 0 : silent + 1;
-        if (silent >= p_.epoch_limit) {
+        if (now - last_rx >= drop_after) {
             lost_ = true;
             cv_.notify_all();
             return;
         }
-        if (!heard) send_raw(heartbeat);
-        heard = false;
-        for (auto& kv : inflight_) {  // resend with capped exponential back-off
-            Out& o = kv.second;
-            if (o.waited >= o.back_off) {
-                o.waited = 0;
-                send_raw(o.bytes);
-                o.back_off = o.back_off == 0 ? std::min(1, p_.max_backoff)
-                                             : std::min(2 * o.back_off, p_.max_backoff);
-            } else {
-                ++o.waited;
+        if (now >= next_tick) {
+            next_tick += epoch;
+            for (auto& kv : inflight_) {  // resend with capped exponential back-off
+                Out& o = kv.second;
+                if (o.waited >= o.back_off) {
+                    o.waited = 0;
+                    send_raw(o.bytes);
+                    o.back_off = o.back_off == 0 ? std::min(1, p_.max_backoff)
+                                                 : std::min(2 * o.back_off, p_.max_backoff);
+                } else {
+                    ++o.waited;
+                }
             }
         }
+        if (now - last_tx_ >= keepalive) send_raw(heartbeat);
     }
 }
 

@@ -20,6 +20,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <map>
@@ -83,6 +84,7 @@ class LspClient {
     std::mutex mu_;
     std::condition_variable cv_;
     bool lost_ = false, stop_ = false;
+    std::chrono::steady_clock::time_point last_tx_;  // last datagram sent (any kind)
     int next_seq_ = 1;                 // next SeqNum to assign
     int expected_ = 1;                 // next SeqNum to deliver
     std::map<int, Out> inflight_;      // sent, not yet acked

@@ -10,9 +10,13 @@ the staff `mtest` binary drives a miner (p1/README.md:139-141):
 * Connect -> Ack(connID, 0), repeated for a duplicate Connect
   (server_impl.go:292-335)
 * Data acked on receipt and delivered in SeqNum order; own Data resent every
-  epoch until acked, WindowSize in flight; heartbeat Ack(connID, 0) after a
-  silent epoch; a client silent for EpochLimit epochs is dropped
-  (server_impl.go:365-420)
+  epoch until acked, WindowSize in flight (server_impl.go:365-392)
+* liveness timers as the reference server keeps them per client
+  (server_impl.go:397-420): any intact message resets them; a reminder
+  Ack(connID, 0) goes out after one epoch with nothing received (and every
+  epoch after that); nothing received for EpochLimit epochs drops the client.
+  heartbeat="spec" instead sends the reminder in every epoch in which the
+  server sent nothing, as the LSP handout words it.
 
 Optional random datagram loss in either direction, like lspnet's
 SetWriteDropPercent/SetReadDropPercent (lspnet/staff.go).
@@ -74,13 +78,17 @@ class _Client:
         self.backlog = []         # (seq, bytes)
         self.pending = {}
         self.ready = queue.Queue()
-        self.heard = True
-        self.silent = 0
+        self.last_rx = time.monotonic()
+        self.remind_at = self.last_rx
+        self.sent = False          # anything sent this epoch (heartbeat="spec")
         self.lost = False
 
 
 class FakeLspServer:
-    def __init__(self, epoch_ms=100, epoch_limit=5, window=1, drop_send=0.0, drop_recv=0.0, seed=0):
+    def __init__(self, epoch_ms=100, epoch_limit=5, window=1, drop_send=0.0, drop_recv=0.0, seed=0,
+                 heartbeat="reference"):
+        assert heartbeat in ("reference", "spec")
+        self.heartbeat = heartbeat
         self.epoch, self.limit, self.window = epoch_ms / 1000.0, epoch_limit, window
         self.drop_send, self.drop_recv = drop_send, drop_recv
         self.rng = random.Random(seed)
@@ -122,6 +130,9 @@ class FakeLspServer:
 
     # -- internals -------------------------------------------------------------
     def _send(self, data: bytes, addr):
+        c = self.by_addr.get(addr)
+        if c is not None:
+            c.sent = True
         if self.drop_send and self.rng.random() < self.drop_send:
             return
         try:
@@ -150,6 +161,7 @@ class FakeLspServer:
                 return
             if data is not None and not (self.drop_recv and self.rng.random() < self.drop_recv):
                 self._handle(data, addr)
+            self._timers()
             if time.monotonic() >= next_epoch:
                 next_epoch += self.epoch
                 self._tick()
@@ -167,15 +179,16 @@ class FakeLspServer:
                 payload = payload[:size]
                 if checksum(conn_id, seq, size, payload) != cs:
                     return
-            if c is not None:
-                c.heard = True
+            if typ == CONNECT and c is None:
+                c = _Client(self.next_id, addr)
+                self.next_id += 1
+                self.by_addr[addr] = c
+                self.by_id[c.conn_id] = c
+                self.new_conns.put(c.conn_id)
+            if c is not None and not c.lost:             # gotMessageChan: reset both timers
+                c.last_rx = time.monotonic()
+                c.remind_at = c.last_rx + self.epoch
             if typ == CONNECT:
-                if c is None:
-                    c = _Client(self.next_id, addr)
-                    self.next_id += 1
-                    self.by_addr[addr] = c
-                    self.by_id[c.conn_id] = c
-                    self.new_conns.put(c.conn_id)
                 self._send(encode(ACK, c.conn_id, 0, None), addr)
             elif c is None:
                 return
@@ -193,17 +206,26 @@ class FakeLspServer:
                 if c.inflight.pop(seq, None) is not None:
                     self._pump(c)
 
+    def _timers(self):
+        """connDropTimer and (reference mode) reminderTimer, server_impl.go:397-420."""
+        now = time.monotonic()
+        with self.lock:
+            for c in self.by_id.values():
+                if c.lost:
+                    continue
+                if now - c.last_rx >= self.epoch * self.limit:
+                    c.lost = True
+                elif self.heartbeat == "reference" and now >= c.remind_at:
+                    self._send(encode(ACK, c.conn_id, 0, None), c.addr)
+                    c.remind_at = now + self.epoch
+
     def _tick(self):
         with self.lock:
             for c in self.by_id.values():
                 if c.lost:
                     continue
-                c.silent = 0 if c.heard else c.silent + 1
-                if c.silent >= self.limit:
-                    c.lost = True
-                    continue
-                if not c.heard:
-                    self._send(encode(ACK, c.conn_id, 0, None), c.addr)
-                c.heard = False
                 for data in c.inflight.values():
                     self._send(data, c.addr)
+                if self.heartbeat == "spec" and not c.sent:
+                    self._send(encode(ACK, c.conn_id, 0, None), c.addr)
+                c.sent = False

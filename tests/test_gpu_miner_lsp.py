@@ -164,7 +164,7 @@ def test_server_sim_reassigns_a_killed_miner(oracle_mod):
         procs[1].wait(timeout=30)
         pending = list(sim.client_request(client, data, lo, up))
         answers, final, dropped = [], None, set()
-        deadline = time.monotonic() + 240
+        deadline = time.monotonic() + 120
         while final is None and time.monotonic() < deadline:
             for c, msg in pending:
                 if c == client:
@@ -187,7 +187,12 @@ def test_server_sim_reassigns_a_killed_miner(oracle_mod):
                 assert err is None and res.Type == bitcoin.Result
                 answers.append((c, (res.Hash, res.Nonce)))
                 pending += sim.miner_result(c, res.Hash, res.Nonce)
-        assert final is not None, "no Result within the deadline"
+        assert final is not None, ("no Result within the deadline", answers, dropped,
+                                   sim.curr and (sim.curr.responsible, sim.curr.responses),
+                                   [(m.miner_id, m.available) for m in sim.miners],
+                                   [m.miner_id for m in sim.dropped],
+                                   {c: srv.is_lost(c) for c in cids}, pending,
+                                   [p.poll() for p in procs])
         assert len(dropped) == 1              # exactly the killed miner
         assert len(answers) == 3              # two own chunks + the reassigned one
         assert final == sm.merge_in_arrival_order([r for _, r in answers])

@@ -120,6 +120,37 @@ def test_client_detects_lost_server(tool):
             p.kill()
 
 
+# "spec" servers beat at epoch ticks only when idle, so their gaps reach two
+# epochs: EpochLimit 2 is borderline there for any client (the reference's
+# 2-epoch drop timer included), hence 3.
+@pytest.mark.parametrize("heartbeat,limit", [("reference", 5), ("reference", 2), ("spec", 5),
+                                             ("spec", 3)])
+def test_idle_connection_stays_alive(tool, heartbeat, limit):
+    """An idle miner waits between client requests for as long as the server is
+    quiet.  Against the reference server's timers (reminder only after a
+    silent epoch, every message resets them) a client that beat every epoch
+    would keep the server silent and drop it; both sides must survive many
+    EpochLimits of idleness."""
+    import time
+    srv = H.FakeLspServer(epoch_ms=40, epoch_limit=limit, heartbeat=heartbeat)
+    env = dict(os.environ, HM_LSP_EPOCH_MS="40", HM_LSP_EPOCH_LIMIT=str(limit))
+    p = subprocess.Popen([tool, "echo", srv.hostport], stdout=subprocess.PIPE, text=True, env=env)
+    try:
+        cid = srv.accept(timeout=30)
+        assert srv.read(cid, timeout=30) == b"hello"
+        time.sleep(40 * 0.040)                          # 40 idle epochs
+        assert p.poll() is None and not srv.is_lost(cid)
+        srv.write(cid, b"ping")
+        assert srv.read(cid, timeout=30) == b"ping"
+        srv.write(cid, b"quit")
+        out, _ = p.communicate(timeout=30)
+        assert p.returncode == 0 and "echoed 1" in out
+    finally:
+        if p.poll() is None:
+            p.kill()
+        srv.close()
+
+
 def test_bitcoin_codec_go_error_semantics(tool):
     # syntax error: Go decodes nothing (checkValid runs first)
     assert run(tool, "bitcoin", '{"Type":1,"Data":"x","Lower":5') == \
