@@ -280,6 +280,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.lane_shift = s.lane_shift;
             ta.loop_shift = s.loop_shift;
             memcpy(ta.trailer_kw, kw, sizeof kw);
+            tiled_loop_sigma0(s, ta.s0_loop);
             const int grid = persistent_grid(
                 ctx, dv, tiled_blocks_per_cu(s.W1, s.straddle, s.trailer), ta.ntasks);
             Launch L;

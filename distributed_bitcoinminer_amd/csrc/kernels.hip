@@ -74,9 +74,16 @@ constexpr int first_vary(uint32_t vm) {
 
 struct State { uint32_t a, b, c, d, e, f, g, h; };
 
-// One round I of a message block whose lane-varying words are VM.
-template <uint32_t VM, int I>
-DEV void round_step(State& s, uint32_t m[16]) {
+// One round I of a message block.  VM marks the message words that vary
+// from one evaluation to the next: across lanes for a one-shot compression,
+// across iterations of the enclosing nonce loop for the tiled kernel (words
+// that vary across lanes but not across the loop are loop-invariant and, as
+// plain C, hoisted out of it).  SW >= 0 names a word whose sigma0 the caller
+// supplies as s0w: sigma0 is XOR-linear, so for a word built from bit-disjoint
+// lane and loop parts, sigma0(lane | loop) = sigma0(lane) ^ sigma0(loop) costs
+// one XOR per iteration instead of four instructions.
+template <uint32_t VM, int SW, int I>
+DEV void round_step(State& s, uint32_t m[16], uint32_t s0w) {
     constexpr uint64_t WV = sched_vary(VM);
     constexpr int F = first_vary(VM);
     uint32_t w;
@@ -88,7 +95,9 @@ DEV void round_step(State& s, uint32_t m[16]) {
         // uniform terms summed first (scalar), lane-varying terms after
         uint32_t u = 0, v = 0;
         const uint32_t t2 = ssig1<v2>(m[(I - 2) & 15]);
-        const uint32_t t15 = ssig0<v15>(m[(I - 15) & 15]);
+        uint32_t t15;
+        if constexpr (I - 15 == SW) t15 = s0w;
+        else t15 = ssig0<v15>(m[(I - 15) & 15]);
         if constexpr (v2) v += t2; else u += t2;
         if constexpr (v7) v += m[(I - 7) & 15]; else u += m[(I - 7) & 15];
         if constexpr (v15) v += t15; else u += t15;
@@ -104,28 +113,42 @@ DEV void round_step(State& s, uint32_t m[16]) {
     s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
 }
 
-template <uint32_t VM, int... I>
-DEV void rounds_seq(State& s, uint32_t m[16], std::integer_sequence<int, I...>) {
-    (round_step<VM, I>(s, m), ...);
+template <uint32_t VM, int SW, int... I>
+DEV void rounds_seq(State& s, uint32_t m[16], uint32_t s0w, std::integer_sequence<int, I...>) {
+    (round_step<VM, SW, I>(s, m, s0w), ...);
 }
 
 // 64 rounds from state s over message m (m is clobbered into the schedule
-// window).  VM marks the words that vary across lanes.  On return s.a = a64,
-// s.b = a63 (= b64), the rest as well.
-template <uint32_t VM>
-DEV void sha_rounds(State& s, uint32_t m[16]) {
-    rounds_seq<VM>(s, m, std::make_integer_sequence<int, 64>{});
+// window).  VM marks the varying words (see round_step), SW/s0w an optional
+// caller-supplied sigma0(m[SW]).  On return s.a = a64, s.b = a63 (= b64),
+// the rest as well.
+template <uint32_t VM, int SW = -1>
+DEV void sha_rounds(State& s, uint32_t m[16], uint32_t s0w = 0) {
+    rounds_seq<VM, SW>(s, m, s0w, std::make_integer_sequence<int, 64>{});
+}
+
+template <int I>
+DEV void round_kw(State& s, uint32_t kw) {
+    // INV_STATE: round 0 of a block whose start state is invariant in the
+    // caller's loop -- plain C lets the compiler hoist its Sigma functions
+    constexpr bool v = I > 0;
+    const uint32_t t1 = s.h + bsig1<v>(s.e) + ch(s.e, s.f, s.g) + kw;
+    const uint32_t t2 = bsig0<v>(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+template <bool INV_STATE, int... I>
+DEV void rounds_kw_seq(State& s, const uint32_t* __restrict__ kw,
+                       std::integer_sequence<int, I...>) {
+    (round_kw<INV_STATE ? I : I + 1>(s, kw[I]), ...);
 }
 
 // 64 rounds over a constant block given as K[i]+W[i] (wave-uniform).
+// INV_STATE: the start state s does not change across the caller's loop.
+template <bool INV_STATE = false>
 DEV void sha_rounds_kw(State& s, const uint32_t* __restrict__ kw) {
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-        const uint32_t t1 = s.h + bsig1(s.e) + ch(s.e, s.f, s.g) + kw[i];
-        const uint32_t t2 = bsig0(s.a) + maj(s.a, s.b, s.c);
-        s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
-        s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
-    }
+    rounds_kw_seq<INV_STATE>(s, kw, std::make_integer_sequence<int, 64>{});
 }
 
 // Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
@@ -226,25 +249,31 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
         const uint32_t X0 = W[W1 - 1] | (uint32_t)(packed >> 32);
         const uint32_t X1 = W[W1] | (uint32_t)packed;
         const uint64_t nbase = (A.tile0 + tile) * A.pow10V + (uint64_t)v * 100u;
+        const uint32_t s0X1 = ssig0<false>(X1);  // lane part of sigma0(W[W1])
 
         for (uint32_t t1 = 0; t1 < 10; ++t1) {
             for (uint32_t t0 = 0; t0 < 10; ++t0) {
                 uint32_t m[16];
 #pragma unroll
                 for (int k = 0; k < 16; ++k) m[k] = W[k];
+                // loop digits: wave-uniform, in bytes that are zero in X1
+                uint32_t L;
                 if constexpr (STRADDLE) {
                     // last digit opens W[W1], the tens digit closes W[W1-1]:
                     // work on W[W1-1] depends on t1 only and is hoisted out
                     // of the t0 loop
                     m[W1 - 1] = X0 + (0x30u + t1);
-                    m[W1] = X1 + ((0x30u + t0) << 24);
+                    L = (0x30u + t0) << 24;
                 } else {
                     m[W1 - 1] = X0;
-                    m[W1] = X1 + ((((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift);
+                    L = (((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift;
                 }
-                constexpr uint32_t VM = (1u << (W1 - 1)) | (1u << W1);
+                m[W1] = X1 | L;
+                // only W[W1] changes from one t0 step to the next
+                constexpr uint32_t VM = 1u << W1;
+                const uint32_t s0w = s0X1 ^ A.s0_loop[t1 * 10u + t0];  // scalar load
                 State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
-                sha_rounds<VM>(s, m);
+                sha_rounds<VM, W1>(s, m, s0w);
                 uint32_t h0, h1;
                 if constexpr (TRAILER) {
                     State o{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
@@ -357,7 +386,7 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
         const uint32_t* __restrict__ kw = A.kwt + (size_t)t_begin * 64;
         for (uint32_t t = t_begin; t < t_end; ++t, kw += 64) {
             State u = cs;
-            sha_rounds_kw(u, kw);
+            sha_rounds_kw<true>(u, kw);
             const uint32_t h0 = u.a + cs.a;
             const bool cand = h0 <= best_hi;
             if (__builtin_amdgcn_ballot_w64(cand)) {

@@ -54,6 +54,7 @@ struct TiledArgs {
     uint32_t lane_shift; // bit offset of the lowest lane digit in the (W[W1-1]:W[W1]) pair
     uint32_t loop_shift; // bit offset of the units loop digit (tens digit at +8)
     uint32_t trailer_kw[64];  // K[i]+W[i] of the constant trailer block (TRAILER only)
+    uint32_t s0_loop[100];    // sigma0 of the loop-digit part of W[W1], index t1*10+t0
 };
 
 // Chained scan (two-block tails whose final block holds only 1..4 digits):

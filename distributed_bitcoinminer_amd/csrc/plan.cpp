@@ -215,6 +215,17 @@ uint64_t host_hash(const uint8_t* msg, uint64_t len, uint64_t nonce) {
     return ((uint64_t)st[0] << 32) | st[1];
 }
 
+void tiled_loop_sigma0(const SegPlan& s, uint32_t out[100]) {
+    for (uint32_t t1 = 0; t1 < 10; ++t1)
+        for (uint32_t t0 = 0; t0 < 10; ++t0) {
+            // the loop digits' bits of W[W1] (hm_tiled_kernel): the units digit
+            // opens the word when the tens digit straddles into W[W1-1]
+            const uint32_t L = s.straddle ? (0x30u + t0) << 24
+                                          : (((0x30u + t1) << 8) | (0x30u + t0)) << s.loop_shift;
+            out[t1 * 10 + t0] = h_rotr(L, 7) ^ h_rotr(L, 18) ^ (L >> 3);
+        }
+}
+
 void trailer_kw(const SegPlan& s, uint32_t kw[64]) {
     uint32_t w[64];
     memset(w, 0, sizeof w);

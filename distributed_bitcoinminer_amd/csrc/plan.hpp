@@ -64,6 +64,9 @@ std::vector<Shard> partition_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, 
                                    bool force_generic);
 // Host SHA-256 of msg ‖ ' ' ‖ decimal(nonce), first 8 bytes big-endian.
 uint64_t host_hash(const uint8_t* msg, uint64_t len, uint64_t nonce);
+// sigma0 of the wave-uniform loop-digit bits of W[W1] for each loop value
+// t1*10+t0 of hm_tiled_kernel (sigma0 is XOR-linear, the lane bits are disjoint).
+void tiled_loop_sigma0(const SegPlan& s, uint32_t out[100]);
 // K[i] + W[i] of the constant trailer block of a trailer segment.
 void trailer_kw(const SegPlan& s, uint32_t kw[64]);
 
