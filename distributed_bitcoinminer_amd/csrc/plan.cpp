@@ -121,15 +121,17 @@ std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, boo
 }
 
 double seg_cost(const SegPlan& s) {
-    // tiled, one block: model cycles by W1 (straddle variants differ by < 1 %)
-    static const double kTiled[14] = {0,    5018, 4972, 4877, 4785, 4691, 4596,
-                                      4502, 4408, 4505, 4541, 4447, 4352, 4258};
+    // Model cycles per 64 nonces of the kernel instantiation's inner loop
+    // (tools/isa_audit.py over the gfx950 ISA, DESIGN.md §4 issue model).
+    // tiled, one block, by W1 (straddle variants differ by < 0.3 %)
+    static const double kTiled[14] = {0,    4985, 4891, 4796, 4702, 4608, 4513,
+                                      4419, 4324, 4457, 4363, 4269, 4174, 4080};
     switch (s.kind) {
         case HM_KIND_TILED:
-            if (s.trailer) return 7780.0;  // digit block + constant trailer block
+            if (s.trailer) return 7680.0;  // digit block + constant trailer block (W1 13..15)
             return kTiled[std::min(std::max(s.W1, 1), 13)];
         case HM_KIND_CHAINED:
-            return 3481.0;  // per-lane block 0; table-driven final block
+            return 3472.0;  // per-lane block 0; table-driven final block
         default:
             // generic: every tail block per lane, no hoisting (estimate)
             return 6000.0 * s.nb;
