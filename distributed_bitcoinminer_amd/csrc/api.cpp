@@ -167,6 +167,16 @@ int persistent_grid(const hm_ctx* ctx, const Device& dv, int per_cu_auto, uint64
     return (int)std::max<uint64_t>(grid, 1);
 }
 
+// Guided task list of a persistent launch over `nunits` work units: the
+// last ~one unit per wave of the grid is split into kSplit tasks.  Returns
+// the task-id count; *nbig = units dequeued whole.
+uint32_t guided_tasks(uint64_t nunits, int grid, uint32_t* nbig) {
+    const uint64_t waves = (uint64_t)grid * (kBlock / kWaveSize);
+    const uint64_t small = std::min<uint64_t>(nunits, waves);
+    *nbig = (uint32_t)(nunits - small);
+    return (uint32_t)(nunits - small + kSplit * small);
+}
+
 // nonces of [t*P, (t+nt)*P - 1] ∩ [lo, hi] (P = nonces per tile)
 uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     const uint64_t a = std::max(s.lo, t * s.pow10V);
@@ -208,13 +218,14 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.pow10f = pow10_u64(s.f);
         ca.seg_lo = s.lo;
         ca.seg_hi = s.hi;
-        ca.ntasks = (uint32_t)(nt * per_tile);
+        const uint64_t nunits = nt * per_tile;
         ca.tpt = s.tpt;
         ca.ntc = s.ntc;
         ca.tch = s.tch;
         ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
         ca.q = s.q;
-        const int grid = persistent_grid(ctx, dv, chained_blocks_per_cu(), ca.ntasks);
+        const int grid = persistent_grid(ctx, dv, chained_blocks_per_cu(), nunits);
+        ca.ntasks = guided_tasks(nunits, grid, &ca.nbig);
         Launch L;
         int rc = next_event(dv, &L.start);
         if (rc) return rc;
@@ -273,7 +284,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.pow10V = s.pow10V;
             ta.seg_lo = s.lo;
             ta.seg_hi = s.hi;
-            ta.ntasks = (uint32_t)(nt * s.tpt);
+            const uint64_t nunits = nt * s.tpt;
             ta.tpt = s.tpt;
             ta.vmax = (uint32_t)(pow10_u64(s.q) - 1);
             ta.q = s.q;
@@ -282,7 +293,8 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             memcpy(ta.trailer_kw, kw, sizeof kw);
             tiled_loop_sigma0(s, ta.s0_loop);
             const int grid = persistent_grid(
-                ctx, dv, tiled_blocks_per_cu(s.W1, s.straddle, s.trailer), ta.ntasks);
+                ctx, dv, tiled_blocks_per_cu(s.W1, s.straddle, s.trailer), nunits);
+            ta.ntasks = guided_tasks(nunits, grid, &ta.nbig);
             Launch L;
             int rc = next_event(dv, &L.start);
             if (rc) return rc;

@@ -227,8 +227,17 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
         if (lane == 0) task = atomicAdd(A.counter, 1u);
         task = uni(task);
         if (task >= A.ntasks) break;
-        const uint32_t tile = task / A.tpt;
-        const uint32_t chunk = task - tile * A.tpt;
+        // guided sizes: whole units first, then tenths (one tens digit each)
+        uint32_t unit = task, t1_begin = 0, t1_end = 10;
+        if (task >= A.nbig) {
+            const uint32_t k = task - A.nbig;
+            const uint32_t u = k / kSplit;
+            unit = A.nbig + u;
+            t1_begin = k - u * kSplit;
+            t1_end = t1_begin + 1;
+        }
+        const uint32_t tile = unit / A.tpt;
+        const uint32_t chunk = unit - tile * A.tpt;
         const uint32_t* __restrict__ R = A.rec + (size_t)tile * kRecWords;
         uint32_t st[8], W[16];
 #pragma unroll
@@ -251,7 +260,7 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
         const uint64_t nbase = (A.tile0 + tile) * A.pow10V + (uint64_t)v * 100u;
         const uint32_t s0X1 = ssig0<false>(X1);  // lane part of sigma0(W[W1])
 
-        for (uint32_t t1 = 0; t1 < 10; ++t1) {
+        for (uint32_t t1 = t1_begin; t1 < t1_end; ++t1) {
             for (uint32_t t0 = 0; t0 < 10; ++t0) {
                 uint32_t m[16];
 #pragma unroll
@@ -351,8 +360,17 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
         if (lane == 0) task = atomicAdd(A.counter, 1u);
         task = uni(task);
         if (task >= A.ntasks) break;
-        const uint32_t tile = task / per_tile;
-        const uint32_t rem = task - tile * per_tile;
+        // guided sizes: whole loop chunks first, then kSplit pieces of each
+        uint32_t unit = task, part = 0, nparts = 1;
+        if (task >= A.nbig) {
+            const uint32_t k = task - A.nbig;
+            const uint32_t u = k / kSplit;
+            unit = A.nbig + u;
+            part = k - u * kSplit;
+            nparts = kSplit;
+        }
+        const uint32_t tile = unit / per_tile;
+        const uint32_t rem = unit - tile * per_tile;
         const uint32_t chunk = rem / A.ntc;
         const uint32_t tc = rem - chunk * A.ntc;
         const uint32_t* __restrict__ R = A.rec + (size_t)tile * kRecWords;
@@ -380,9 +398,11 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
         const State cs{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
                        s.e + st[4], s.f + st[5], s.g + st[6], s.h + st[7]};
         const uint64_t nbase = (A.tile0 + tile) * A.pow10qf + (uint64_t)v * A.pow10f;
-        const uint32_t t_begin = tc * A.tch;
-        uint32_t t_end = t_begin + A.tch;
+        const uint32_t piece = (A.tch + nparts - 1) / nparts;
+        const uint32_t t_begin = tc * A.tch + part * piece;
+        uint32_t t_end = tc * A.tch + A.tch;
         if (t_end > (uint32_t)A.pow10f) t_end = (uint32_t)A.pow10f;
+        if (t_end > t_begin + piece) t_end = t_begin + piece;
         const uint32_t* __restrict__ kw = A.kwt + (size_t)t_begin * 64;
         for (uint32_t t = t_begin; t < t_end; ++t, kw += 64) {
             State u = cs;

@@ -22,6 +22,11 @@ constexpr int kRecWords = 32;          // tile record stride: state[8], W[16], p
 constexpr uint32_t kMaxTilesPerLaunch = 1u << 20;
 constexpr uint32_t kMaxCandWaves = 32768;  // per-launch candidate slots (waves)
 constexpr int kMaxBatch = 64;              // requests per hm_scan_many chunk
+// Guided task sizes: a launch's first `nbig` work units are dequeued whole,
+// the last ones (about one per wave of the grid) as kSplit tasks of a tenth
+// of the loop each, so waves that finish early pick up small pieces and the
+// launch's tail shrinks ~10x.
+constexpr uint32_t kSplit = 10;
 
 // Tile planner: one thread per tile.
 struct PlanArgs {
@@ -47,8 +52,9 @@ struct TiledArgs {
     uint64_t tile0;
     uint64_t pow10V;
     uint64_t seg_lo, seg_hi;
-    uint32_t ntasks;
-    uint32_t tpt;        // tasks per tile = ceil(10^q / 64)
+    uint32_t ntasks;     // task ids: nbig whole units, then kSplit per remaining unit
+    uint32_t nbig;       // units dequeued whole (all 100 loop steps)
+    uint32_t tpt;        // units (64-lane chunks) per tile = ceil(10^q / 64)
     uint32_t vmax;       // 10^q - 1
     uint32_t q;          // lane digits
     uint32_t lane_shift; // bit offset of the lowest lane digit in the (W[W1-1]:W[W1]) pair
@@ -72,7 +78,8 @@ struct ChainedArgs {
     uint64_t pow10qf;        // nonces per tile = 10^(q+f)
     uint64_t pow10f;         // loop values = 10^f
     uint64_t seg_lo, seg_hi;
-    uint32_t ntasks;
+    uint32_t ntasks;         // task ids: nbig whole units, then kSplit per remaining unit
+    uint32_t nbig;           // units (lane chunk x loop chunk) dequeued whole
     uint32_t tpt;            // lane chunks per tile = ceil(10^q / 64)
     uint32_t ntc;            // loop chunks per lane chunk
     uint32_t tch;            // loop values per loop chunk
