@@ -88,6 +88,11 @@ def load() -> ctypes.CDLL:
         lib.hm_scan_many.restype = ctypes.c_int
         lib.hm_scan_many.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_request), ctypes.c_int,
                                      ctypes.POINTER(hm_result)]
+        lib.hm_scan_checked.restype = ctypes.c_int
+        lib.hm_scan_checked.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.POINTER(hm_result),
+                                        ctypes.POINTER(ctypes.c_uint64),
+                                        ctypes.POINTER(ctypes.c_uint64)]
         lib.hm_scan_stats.restype = ctypes.c_int
         lib.hm_scan_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats)]
         lib.hm_set_option.restype = ctypes.c_int
@@ -147,6 +152,17 @@ class Context:
         if rc != HM_OK:
             raise HipMinerError(rc, "hm_scan")
         return int(out.hash), int(out.nonce)
+
+    def scan_checked(self, msg, lo: int, hi: int) -> tuple[tuple[int, int], int, int]:
+        """hm_scan_checked: ((hash, nonce), sum of all keys mod 2^64, nonces hashed)."""
+        m = as_bytes(msg)
+        out = hm_result()
+        s, c = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self._lib.hm_scan_checked(self._h, m, len(m), lo, hi, ctypes.byref(out),
+                                       ctypes.byref(s), ctypes.byref(c))
+        if rc != HM_OK:
+            raise HipMinerError(rc, "hm_scan_checked")
+        return (int(out.hash), int(out.nonce)), int(s.value), int(c.value)
 
     def scan_many(self, requests) -> list[tuple[int, int]]:
         """hm_scan_many over [(msg, lo, hi), ...]."""

@@ -44,9 +44,9 @@ struct Launch {
     char kernel[64];  // kernel instantiation, as rocprofv3 names it (sans args)
 };
 
-void name_tiled(char* out, const SegPlan& s) {
-    snprintf(out, 64, "hm_tiled_kernel<%d, %s, %s>", s.W1, s.straddle ? "true" : "false",
-             s.trailer ? "true" : "false");
+void name_tiled(char* out, const SegPlan& s, bool csum) {
+    snprintf(out, 64, "%s<%d, %s, %s>", csum ? "hm_tiled_csum_kernel" : "hm_tiled_kernel", s.W1,
+             s.straddle ? "true" : "false", s.trailer ? "true" : "false");
 }
 
 struct Device {
@@ -57,6 +57,8 @@ struct Device {
     uint32_t* kwt[kStreams] = {};
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
+    uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
+    uint64_t* acc = nullptr;        // checked scans: [kStreams][2] (sum, count)
     uint64_t* best = nullptr;      // [kMaxBatch][kStreams][2]: per request, per stream
     uint64_t* result = nullptr;    // [kMaxBatch][2]
     uint64_t* gathered = nullptr;  // [ndev][kMaxBatch][2] (RCCL merge)
@@ -93,6 +95,7 @@ struct hm_ctx {
     bool merge_rccl = false;
     int grid_per_cu = 0;
     int streams = 1;
+    bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
     bool have_stats = false;
     hm_stats last{};
 };
@@ -121,9 +124,11 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
+        HIPCHK(hipMalloc(&dv.sums[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
     }
     HIPCHK(hipMalloc(&dv.best, (size_t)kMaxBatch * kStreams * 2 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&dv.acc, (size_t)kStreams * 2 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&dv.result, (size_t)kMaxBatch * 2 * sizeof(uint64_t)));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), kMaxBatch * sizeof(hm_result)));
     return HM_OK;
@@ -141,11 +146,13 @@ void device_free(Device& dv) {
         if (dv.cand[s]) (void)hipFree(dv.cand[s]);
         if (dv.kwt[s]) (void)hipFree(dv.kwt[s]);
         if (dv.counter[s]) (void)hipFree(dv.counter[s]);
+        if (dv.sums[s]) (void)hipFree(dv.sums[s]);
         if (dv.join[s]) (void)hipEventDestroy(dv.join[s]);
         if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
     }
     for (hipEvent_t e : dv.evpool) (void)hipEventDestroy(e);
     if (dv.best) (void)hipFree(dv.best);
+    if (dv.acc) (void)hipFree(dv.acc);
     if (dv.result) (void)hipFree(dv.result);
     if (dv.gathered) (void)hipFree(dv.gathered);
     if (dv.host_out) (void)hipHostFree(dv.host_out);
@@ -213,6 +220,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.kwt = dv.kwt[si];
         ca.counter = dv.counter[si];
         ca.cand = dv.cand[si];
+        ca.sums = ctx->csum ? dv.sums[si] : nullptr;
         ca.tile0 = t;
         ca.pow10qf = s.pow10V;
         ca.pow10f = pow10_u64(s.f);
@@ -233,14 +241,17 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         if (rc) return rc;
         L.nonces = tile_span_nonces(s, t, nt);
         L.kind = HM_KIND_CHAINED;
-        snprintf(L.kernel, sizeof L.kernel, "hm_chained_kernel");
+        snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
         L.grid = grid;
         L.compressions = count_compressions(s);
         HIPCHK(hipEventRecord(L.start, st));
-        HIPCHK(launch_chained(ca, grid, st));
+        HIPCHK(launch_chained(ca, grid, st, ctx->csum));
         HIPCHK(hipEventRecord(L.stop, st));
         HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si,
                            st));
+        if (ctx->csum)
+            HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize),
+                                   dv.acc + 2 * si, st));
         dv.launches.push_back(L);
         t += nt;
         if (t == 0) break;
@@ -280,6 +291,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.rec = dv.rec[si];
             ta.counter = dv.counter[si];
             ta.cand = dv.cand[si];
+            ta.sums = ctx->csum ? dv.sums[si] : nullptr;
             ta.tile0 = t;
             ta.pow10V = s.pow10V;
             ta.seg_lo = s.lo;
@@ -302,14 +314,17 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             if (rc) return rc;
             L.nonces = tile_span_nonces(s, t, nt);
             L.kind = HM_KIND_TILED;
-            name_tiled(L.kernel, s);
+            name_tiled(L.kernel, s, ctx->csum);
             L.grid = grid;
             L.compressions = count_compressions(s);
             HIPCHK(hipEventRecord(L.start, st));
-            HIPCHK(launch_tiled(ta, s.W1, s.straddle, s.trailer, grid, st));
+            HIPCHK(launch_tiled(ta, s.W1, s.straddle, s.trailer, grid, st, ctx->csum));
             HIPCHK(hipEventRecord(L.stop, st));
             HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize),
                                best + 2 * si, st));
+            if (ctx->csum)
+                HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize),
+                                       dv.acc + 2 * si, st));
             dv.launches.push_back(L);
             t += nt;
             if (t == 0) break;  // tile index wrapped (cannot happen for d <= 20)
@@ -319,6 +334,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     // generic
     GenericArgs ga;
     ga.cand = dv.cand[si];
+    ga.sums = ctx->csum ? dv.sums[si] : nullptr;
     ga.seg_lo = s.lo;
     ga.count_m1 = s.hi - s.lo;
     ga.total_bits = s.total_bits;
@@ -337,13 +353,16 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     if (rc) return rc;
     L.nonces = ga.count_m1 + 1;  // generic segments are far below 2^64
     L.kind = HM_KIND_GENERIC;
-    snprintf(L.kernel, sizeof L.kernel, "hm_generic_kernel");
+    snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_generic_csum_kernel" : "hm_generic_kernel");
     L.grid = grid;
     L.compressions = count_compressions(s);
     HIPCHK(hipEventRecord(L.start, st));
-    HIPCHK(launch_generic(ga, grid, st));
+    HIPCHK(launch_generic(ga, grid, st, ctx->csum));
     HIPCHK(hipEventRecord(L.stop, st));
     HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si, st));
+    if (ctx->csum)
+        HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize),
+                               dv.acc + 2 * si, st));
     dv.launches.push_back(L);
     return HM_OK;
 }
@@ -362,6 +381,7 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     hipStream_t s0 = dv.stream[0];
     HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
     HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
+    if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
     HIPCHK(hipEventRecord(dv.join[0], s0));
     for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
     // streams == 1 (default): every segment in order on stream 0, so kernels
@@ -495,7 +515,8 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
     return host_hash(msg ? msg : &empty, msg ? len : 0, nonce);
 }
 
-int hm_version(void) { return (1 << 16) | 2; }  // 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition
+// 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked
+int hm_version(void) { return (1 << 16) | 3; }
 
 int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t* bounds) {
@@ -579,11 +600,12 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
     }
 }
 
-int hm_scan_many(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
-    if (!ctx || n < 0 || (n > 0 && (!reqs || !outs))) return HM_ERR_INVALID;
-    for (int r = 0; r < n; ++r)
-        if (!reqs[r].msg && reqs[r].len) return HM_ERR_INVALID;
-    std::lock_guard<std::mutex> g(ctx->mu);
+}  // extern "C"
+
+namespace {
+
+// hm_scan_many with ctx->mu held.
+int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<hm_result> res(n);
     for (auto& dv : ctx->devs) {
@@ -644,11 +666,46 @@ int hm_scan_many(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
     return HM_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int hm_scan_many(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
+    if (!ctx || n < 0 || (n > 0 && (!reqs || !outs))) return HM_ERR_INVALID;
+    for (int r = 0; r < n; ++r)
+        if (!reqs[r].msg && reqs[r].len) return HM_ERR_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return scan_many_locked(ctx, reqs, n, outs);
+}
+
 int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
             hm_result* out) {
     if (!ctx || !out || (!msg && len)) return HM_ERR_INVALID;
     hm_request q{msg, len, lo, hi};
     return hm_scan_many(ctx, &q, 1, out);
+}
+
+int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
+                    hm_result* out, uint64_t* sum, uint64_t* count) {
+    if (!ctx || !out || !sum || !count || (!msg && len)) return HM_ERR_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    hm_request q{msg, len, lo, hi};
+    hm_result res;
+    ctx->csum = true;
+    int rc = scan_many_locked(ctx, &q, 1, &res);
+    ctx->csum = false;
+    if (rc) return rc;
+    uint64_t s = 0, c = 0;
+    for (auto& dv : ctx->devs) {
+        uint64_t a[kStreams * 2];
+        HIPCHK(hipSetDevice(dv.ordinal));
+        HIPCHK(hipMemcpy(a, dv.acc, sizeof a, hipMemcpyDeviceToHost));
+        for (int i = 0; i < kStreams; ++i) { s += a[2 * i]; c += a[2 * i + 1]; }
+    }
+    *out = res;
+    *sum = s;
+    *count = c;
+    return HM_OK;
 }
 
 

@@ -13,11 +13,18 @@
 //                        padding spills); wave-uniform running min in SGPRs,
 //                        refreshed by a 64-lane shuffle reduce only when some
 //                        lane's H0 <= the wave's best H0.
+//   hm_chained_kernel    two-block tails whose final block is wave-uniform:
+//                        per lane block 0 once, then a table-driven block.
 //   hm_generic_kernel    one nonce per lane with a byte-level tail builder;
 //                        small or irregular segments and cross-checks.
 //   hm_fold_kernel       second reduce pass (candidates -> 16-B best).
+//   hm_*_csum_kernel     checked variants of the three scan kernels (same
+//                        body, CSUM=true): also the wrapping sum of the keys
+//                        and the count of nonces hashed, per wave, folded by
+//                        hm_sum_fold_kernel (hm_scan_checked).
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <utility>
 
 #include "kernels.hpp"
@@ -163,6 +170,23 @@ DEV void wave_min(uint64_t& k, uint64_t& n) {
     }
 }
 
+// Wrapping sum across the 64 lanes; every lane gets it.
+DEV uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, kWaveSize);
+    return x;
+}
+
+// Checked scans: lane 0 stores the wave's (sum of keys, count) coverage pair.
+DEV void store_sums(uint64_t* sums, uint32_t wslot, uint64_t sum, uint64_t cnt) {
+    sum = wave_sum(sum);
+    cnt = wave_sum(cnt);
+    if (__lane_id() == 0) {
+        sums[2 * wslot] = sum;
+        sums[2 * wslot + 1] = cnt;
+    }
+}
+
 DEV void put_byte(uint32_t* w, uint32_t pos, uint32_t byte) {
     w[pos >> 2] |= byte << (24u - 8u * (pos & 3u));
 }
@@ -214,13 +238,15 @@ __global__ void __launch_bounds__(kBlock) hm_tile_plan_kernel(const PlanArgs A) 
 #define HM_TILED_BOUNDS __launch_bounds__(kBlock)
 #endif
 
-template <int W1, bool STRADDLE, bool TRAILER>
-__global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
+// CSUM: checked variant (coverage sum and count of the hashed keys).
+template <int W1, bool STRADDLE, bool TRAILER, bool CSUM>
+DEV void tiled_body(const TiledArgs& A) {
     static_assert(W1 >= 1 && W1 <= 15, "varying words are W[W1-1], W[W1]");
     const uint32_t lane = __lane_id();
     const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
     uint32_t best_hi = 0xffffffffu, best_lo = 0xffffffffu;  // wave-uniform (SGPR)
     uint64_t best_nonce = 0;
+    uint64_t csum = 0, ccnt = 0;  // CSUM only
 
     for (;;) {
         uint32_t task = 0;
@@ -246,6 +272,7 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
         for (int k = 0; k < 16; ++k) W[k] = R[8 + k];
 
         uint32_t v = chunk * kWaveSize + lane;
+        const bool lane_ok = v <= A.vmax;  // CSUM: surplus lanes are not counted
         v = v > A.vmax ? A.vmax : v;  // surplus lanes repeat a valid nonce
         uint64_t packed = 0;
         uint32_t x = v;
@@ -295,6 +322,13 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
                     h0 = s.a + st[0];
                     h1 = s.b + st[1];
                 }
+                if constexpr (CSUM) {
+                    const uint64_t n = nbase + t1 * 10u + t0;
+                    if (lane_ok && n >= A.seg_lo && n <= A.seg_hi) {
+                        csum += ((uint64_t)h0 << 32) | h1;
+                        ++ccnt;
+                    }
+                }
                 const bool cand = h0 <= best_hi;
                 if (__builtin_amdgcn_ballot_w64(cand)) {
                     // rare: some lane may beat the wave's best
@@ -319,6 +353,17 @@ __global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
         A.cand[2 * wslot] = ((uint64_t)best_hi << 32) | best_lo;
         A.cand[2 * wslot + 1] = best_nonce;
     }
+    if constexpr (CSUM) store_sums(A.sums, wslot, csum, ccnt);
+}
+
+template <int W1, bool STRADDLE, bool TRAILER>
+__global__ void HM_TILED_BOUNDS hm_tiled_kernel(const TiledArgs A) {
+    tiled_body<W1, STRADDLE, TRAILER, false>(A);
+}
+
+template <int W1, bool STRADDLE, bool TRAILER>
+__global__ void HM_TILED_BOUNDS hm_tiled_csum_kernel(const TiledArgs A) {
+    tiled_body<W1, STRADDLE, TRAILER, true>(A);
 }
 
 // ---------------------------------------------------------------------------
@@ -348,11 +393,13 @@ __global__ void __launch_bounds__(kBlock) hm_kw_table_kernel(uint32_t* __restric
     for (int k = 0; k < 64; ++k) o[k] = kK[k] + w[k];
 }
 
-__global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A) {
+template <bool CSUM>
+DEV void chained_body(const ChainedArgs& A) {
     const uint32_t lane = __lane_id();
     const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
     uint32_t best_hi = 0xffffffffu, best_lo = 0xffffffffu;
     uint64_t best_nonce = 0;
+    uint64_t csum = 0, ccnt = 0;  // CSUM only
     const uint32_t per_tile = A.tpt * A.ntc;
 
     for (;;) {
@@ -381,6 +428,7 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
         for (int k = 0; k < 16; ++k) W[k] = R[8 + k];
 
         uint32_t v = chunk * kWaveSize + lane;
+        const bool lane_ok = v <= A.vmax;
         v = v > A.vmax ? A.vmax : v;
         uint32_t packed = 0, x = v;
         for (uint32_t k = 0; k < A.q; ++k) {
@@ -408,6 +456,13 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
             State u = cs;
             sha_rounds_kw<true>(u, kw);
             const uint32_t h0 = u.a + cs.a;
+            if constexpr (CSUM) {
+                const uint64_t n = nbase + t;
+                if (lane_ok && n >= A.seg_lo && n <= A.seg_hi) {
+                    csum += ((uint64_t)h0 << 32) | (u.b + cs.b);
+                    ++ccnt;
+                }
+            }
             const bool cand = h0 <= best_hi;
             if (__builtin_amdgcn_ballot_w64(cand)) {
                 uint64_t key = ((uint64_t)h0 << 32) | (u.b + cs.b);
@@ -430,14 +485,25 @@ __global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A)
         A.cand[2 * wslot] = ((uint64_t)best_hi << 32) | best_lo;
         A.cand[2 * wslot + 1] = best_nonce;
     }
+    if constexpr (CSUM) store_sums(A.sums, wslot, csum, ccnt);
+}
+
+__global__ void __launch_bounds__(kBlock) hm_chained_kernel(const ChainedArgs A) {
+    chained_body<false>(A);
+}
+
+__global__ void __launch_bounds__(kBlock) hm_chained_csum_kernel(const ChainedArgs A) {
+    chained_body<true>(A);
 }
 
 // ---------------------------------------------------------------------------
 // Generic scan: one nonce per lane, any layout
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A) {
+template <bool CSUM>
+DEV void generic_body(const GenericArgs& A) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t bk = ~0ull, bn = 0;
+    uint64_t csum = 0, ccnt = 0;  // CSUM only
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.count_m1;) {
         const uint64_t n = A.seg_lo + k;
         uint32_t w[32];
@@ -458,16 +524,26 @@ __global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A)
         h_compress(st, w);
         if (A.nb == 2) h_compress(st, w + 16);
         const uint64_t key = ((uint64_t)st[0] << 32) | st[1];
+        if constexpr (CSUM) { csum += key; ++ccnt; }
         if (key < bk || (key == bk && n < bn)) { bk = key; bn = n; }
         if (A.count_m1 - k < stride) break;
         k += stride;
     }
     wave_min(bk, bn);
+    const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + threadIdx.x / kWaveSize;
     if (__lane_id() == 0) {
-        const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + threadIdx.x / kWaveSize;
         A.cand[2 * wslot] = bk;
         A.cand[2 * wslot + 1] = bn;
     }
+    if constexpr (CSUM) store_sums(A.sums, wslot, csum, ccnt);
+}
+
+__global__ void __launch_bounds__(kBlock) hm_generic_kernel(const GenericArgs A) {
+    generic_body<false>(A);
+}
+
+__global__ void __launch_bounds__(kBlock) hm_generic_csum_kernel(const GenericArgs A) {
+    generic_body<true>(A);
 }
 
 // ---------------------------------------------------------------------------
@@ -494,6 +570,25 @@ __global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restr
     }
 }
 
+__global__ void __launch_bounds__(kBlock) hm_sum_fold_kernel(const uint64_t* __restrict__ sums,
+                                                             uint32_t n, uint64_t* acc) {
+    __shared__ uint64_t ss[kBlock / kWaveSize], sc[kBlock / kWaveSize];
+    uint64_t a = 0, c = 0;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        a += sums[2 * (size_t)i];
+        c += sums[2 * (size_t)i + 1];
+    }
+    a = wave_sum(a);
+    c = wave_sum(c);
+    if (__lane_id() == 0) { ss[threadIdx.x / kWaveSize] = a; sc[threadIdx.x / kWaveSize] = c; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / kWaveSize; ++w) { a += ss[w]; c += sc[w]; }
+        acc[0] += a;
+        acc[1] += c;
+    }
+}
+
 __global__ void hm_init_best_kernel(uint64_t* best, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) { best[2 * i] = ~0ull; best[2 * i + 1] = 0; }  // (MaxUint64, 0): miner.go:65-66
@@ -510,34 +605,44 @@ hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s) {
 
 using TiledFn = void (*)(const TiledArgs);
 
-#define HM_T(W, S, T) &hm_tiled_kernel<W, S, T>
-// [trailer][straddle][W1]; nullptr = layout that cannot occur
-static const TiledFn kTiled[2][2][16] = {
-    {{nullptr, HM_T(1, false, false), HM_T(2, false, false), HM_T(3, false, false),
-      HM_T(4, false, false), HM_T(5, false, false), HM_T(6, false, false), HM_T(7, false, false),
-      HM_T(8, false, false), HM_T(9, false, false), HM_T(10, false, false),
-      HM_T(11, false, false), HM_T(12, false, false), HM_T(13, false, false), nullptr, nullptr},
-     {nullptr, HM_T(1, true, false), HM_T(2, true, false), HM_T(3, true, false),
-      HM_T(4, true, false), HM_T(5, true, false), HM_T(6, true, false), HM_T(7, true, false),
-      HM_T(8, true, false), HM_T(9, true, false), HM_T(10, true, false), HM_T(11, true, false),
-      HM_T(12, true, false), HM_T(13, true, false), nullptr, nullptr}},
-    {{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-      nullptr, nullptr, nullptr, HM_T(13, false, true), HM_T(14, false, true),
-      HM_T(15, false, true)},
-     {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-      nullptr, nullptr, nullptr, HM_T(13, true, true), HM_T(14, true, true),
-      HM_T(15, true, true)}}};
-#undef HM_T
+// Instantiated layouts: one tail block W1 1..13, or W1 13..15 with a constant
+// trailer block; nullptr = a layout that cannot occur.
+template <int W, bool S, bool T, bool C>
+constexpr TiledFn tiled_ptr() {
+    if constexpr (W >= 1 && W <= 15 && (T ? W >= 13 : W <= 13)) {
+        if constexpr (C) return &hm_tiled_csum_kernel<W, S, T>;
+        else return &hm_tiled_kernel<W, S, T>;
+    } else {
+        return nullptr;
+    }
+}
 
-static TiledFn tiled_fn(int W1, bool straddle, bool trailer) {
+template <bool S, bool T, bool C, int... W>
+constexpr std::array<TiledFn, 16> tiled_row(std::integer_sequence<int, W...>) {
+    return {{tiled_ptr<W, S, T, C>()...}};
+}
+
+template <bool S, bool T, bool C>
+constexpr std::array<TiledFn, 16> tiled_row() {
+    return tiled_row<S, T, C>(std::make_integer_sequence<int, 16>{});
+}
+
+// [csum][trailer][straddle][W1]
+static const std::array<TiledFn, 16> kTiled[2][2][2] = {
+    {{tiled_row<false, false, false>(), tiled_row<true, false, false>()},
+     {tiled_row<false, true, false>(), tiled_row<true, true, false>()}},
+    {{tiled_row<false, false, true>(), tiled_row<true, false, true>()},
+     {tiled_row<false, true, true>(), tiled_row<true, true, true>()}}};
+
+static TiledFn tiled_fn(int W1, bool straddle, bool trailer, bool csum = false) {
     if (W1 < 1 || W1 > 15) return nullptr;
-    return kTiled[trailer ? 1 : 0][straddle ? 1 : 0][W1];
+    return kTiled[csum ? 1 : 0][trailer ? 1 : 0][straddle ? 1 : 0][W1];
 }
 
 hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
-                        hipStream_t s) {
-    TiledFn fn = tiled_fn(W1, straddle, trailer);
-    if (!fn) return hipErrorInvalidValue;
+                        hipStream_t s, bool csum) {
+    TiledFn fn = tiled_fn(W1, straddle, trailer, csum);
+    if (!fn || (csum && !a.sums)) return hipErrorInvalidValue;
     if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kBlock), 0, s, a);
@@ -554,17 +659,26 @@ int tiled_blocks_per_cu(int W1, bool straddle, bool trailer) {
     return nb;
 }
 
-hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s) {
-    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s, bool csum) {
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves ||
+        (csum && !a.sums))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(hm_generic_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    if (csum) hipLaunchKernelGGL(hm_generic_csum_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(hm_generic_kernel, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s) {
-    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s, bool csum) {
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves ||
+        (csum && !a.sums))
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(hm_chained_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    if (csum) hipLaunchKernelGGL(hm_chained_csum_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    else hipLaunchKernelGGL(hm_chained_kernel, dim3(grid), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipStream_t s) {
+    hipLaunchKernelGGL(hm_sum_fold_kernel, dim3(1), dim3(kBlock), 0, s, sums, n, acc);
     return hipGetLastError();
 }
 

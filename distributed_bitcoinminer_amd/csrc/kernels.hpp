@@ -49,6 +49,7 @@ struct TiledArgs {
     const uint32_t* rec;
     unsigned int* counter;
     uint64_t* cand;      // 2 x u64 per wave slot: (key, nonce)
+    uint64_t* sums;      // checked scans only: 2 x u64 per wave slot (sum of keys, count)
     uint64_t tile0;
     uint64_t pow10V;
     uint64_t seg_lo, seg_hi;
@@ -74,6 +75,7 @@ struct ChainedArgs {
     const uint32_t* kwt;     // [10^f][64] K+W of the final block per loop value
     unsigned int* counter;
     uint64_t* cand;
+    uint64_t* sums;          // checked scans only (see TiledArgs)
     uint64_t tile0;
     uint64_t pow10qf;        // nonces per tile = 10^(q+f)
     uint64_t pow10f;         // loop values = 10^f
@@ -90,6 +92,7 @@ struct ChainedArgs {
 // Generic scan: one nonce per lane (small / irregular segments, cross-checks).
 struct GenericArgs {
     uint64_t* cand;
+    uint64_t* sums;      // checked scans only (see TiledArgs)
     uint64_t seg_lo;
     uint64_t count_m1;   // nonces - 1
     uint64_t total_bits;
@@ -103,10 +106,17 @@ hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s);
 // W1 in [1, 15], straddle: loop tens digit in W[W1-1], trailer: constant
 // final block after the digit block.  Returns hipErrorInvalidValue for an
 // unsupported combination.
+//
+// csum: the checked variant (hm_*_csum_kernel) of the same kernel.  It also
+// accumulates, per wave, the wrapping sum of the keys and the count of the
+// in-range nonces it hashed into a.sums -- the coverage checksum of
+// hm_scan_checked (every nonce of [lo, hi] hashed exactly once).
 hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
-                        hipStream_t s);
-hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s);
-hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s);
+                        hipStream_t s, bool csum = false);
+hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s, bool csum = false);
+hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s, bool csum = false);
+// acc[0] += sum of sums[2i], acc[1] += sum of sums[2i+1] for i < n (wrapping).
+hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipStream_t s);
 int chained_blocks_per_cu();
 // K+W table of the final block for loop values t in [0, 10^f).
 hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s);

@@ -75,6 +75,23 @@ type Request struct {
 	Lo, Hi uint64
 }
 
+// ScanChecked is ScanInclusive plus the coverage checksum of
+// hm_scan_checked: the sum of every key in [lo, hi] mod 2^64 and the number
+// of nonces hashed.  For verification runs; slower than ScanInclusive.
+func (m *Miner) ScanChecked(data string, lo, hi uint64) (hash, nonce, sum, count uint64, err error) {
+	var out C.hm_result
+	var s, c C.uint64_t
+	var p *C.uint8_t
+	if len(data) > 0 {
+		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
+	}
+	rc := C.hm_scan_checked(m.ctx, p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi), &out, &s, &c)
+	if rc != 0 {
+		return 0, 0, 0, 0, Error{int(rc)}
+	}
+	return uint64(out.hash), uint64(out.nonce), uint64(s), uint64(c), nil
+}
+
 // ScanMany runs hm_scan_many: every request's GPU work is queued before one
 // synchronisation.  Results are in request order.
 func (m *Miner) ScanMany(reqs []Request) ([][2]uint64, error) {

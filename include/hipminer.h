@@ -128,6 +128,18 @@ typedef struct hm_request {
  * batch them here).  outs is written only when the call returns HM_OK. */
 int hm_scan_many(hm_ctx *ctx, const hm_request *reqs, int n, hm_result *outs);
 
+/* Checked scan: hm_scan's result plus a coverage checksum computed on the GPU
+ * by the checked variants of the same kernels (same planner, tiles, lane and
+ * loop layout, guided task split and multi-device shards):
+ *   *sum   = sum over n in [lo, hi] of Hash(msg, n), mod 2^64
+ *   *count = number of nonces hashed (must be hi - lo + 1, mod 2^64)
+ * A nonce skipped, hashed twice or hashed with wrong bytes changes the pair,
+ * so it checks coverage at sizes no CPU can rescan; the sums of disjoint
+ * sub-ranges add up to the sum of their union.  A verification entry point,
+ * not the hot path: it runs slower than hm_scan. */
+int hm_scan_checked(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi,
+                    hm_result *out, uint64_t *sum, uint64_t *count);
+
 /* Split the inclusive range [lo, hi] into n contiguous, ascending shards of
  * near-equal modelled GPU cost for msg (digit segments whose kernels cost more
  * per nonce get fewer nonces).  bounds[2i], bounds[2i+1] = shard

@@ -133,17 +133,20 @@ typedef struct {
     uint64_t lo, hi; /* inclusive */
     int empty;
     uint64_t hash, nonce;
+    uint64_t sum, count; /* coverage checksum: wrapping sum of keys, nonces hashed */
 } o_job;
 
 /* miner.go:65-76 over inclusive [lo, hi], strict <, ascending. */
 static void *o_scan_job(void *arg) {
     o_job *j = (o_job *)arg;
-    uint64_t result = MAXU64, index = 0;
+    uint64_t result = MAXU64, index = 0, sum = 0, count = 0;
     if (!j->empty) {
         uint8_t *buf = (uint8_t *)malloc(j->len + 32);
         uint64_t i = j->lo;
         for (;;) {
             uint64_t h = o_hash_buf(j->msg, j->len, i, buf);
+            sum += h;
+            count++;
             if (h < result) { result = h; index = i; }
             if (i == j->hi) break;
             i++;
@@ -152,13 +155,20 @@ static void *o_scan_job(void *arg) {
     }
     j->hash = result;
     j->nonce = index;
+    j->sum = sum;
+    j->count = count;
     return NULL;
 }
 
 /* Inclusive scan [lo, hi] (hi may be 2^64-1).  lo > hi is an empty range and
- * returns (MaxUint64, 0), the miner's initial value (miner.go:65-66). */
-void oracle_scan(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int threads,
-                 uint64_t *out_hash, uint64_t *out_nonce) {
+ * returns (MaxUint64, 0), the miner's initial value (miner.go:65-66).
+ * Also returns the coverage checksum that hm_scan_checked computes on the
+ * GPU: the wrapping (mod 2^64) sum of every key and the number of nonces. */
+void oracle_scan_sum(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int threads,
+                     uint64_t *out_hash, uint64_t *out_nonce, uint64_t *out_sum,
+                     uint64_t *out_count) {
+    *out_sum = 0;
+    *out_count = 0;
     if (lo > hi) { *out_hash = MAXU64; *out_nonce = 0; return; }
     if (threads < 1) threads = 1;
     uint64_t span_m1 = hi - lo; /* count - 1, never overflows */
@@ -181,12 +191,21 @@ void oracle_scan(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int t
         for (int c = 0; c < threads; c++) pthread_create(&tids[c], NULL, o_scan_job, &jobs[c]);
         for (int c = 0; c < threads; c++) pthread_join(tids[c], NULL);
     }
-    uint64_t bh = MAXU64, bn = 0;
+    uint64_t bh = MAXU64, bn = 0, bs = 0, bc = 0;
     for (int c = 0; c < threads; c++) { /* chunks ascend: strict < keeps lowest nonce */
         if (jobs[c].hash < bh) { bh = jobs[c].hash; bn = jobs[c].nonce; }
+        bs += jobs[c].sum;
+        bc += jobs[c].count;
     }
     *out_hash = bh; *out_nonce = bn;
+    *out_sum = bs; *out_count = bc;
     free(jobs); free(tids);
+}
+
+void oracle_scan(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int threads,
+                 uint64_t *out_hash, uint64_t *out_nonce) {
+    uint64_t s, c;
+    oracle_scan_sum(msg, len, lo, hi, threads, out_hash, out_nonce, &s, &c);
 }
 
 /* miner.go:67-76 verbatim semantics, including `upper := Upper + 1` wrapping

@@ -47,6 +47,10 @@ def _load():
             fn.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                            ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
                            ctypes.POINTER(ctypes.c_uint64)]
+        lib.oracle_scan_sum.restype = None
+        lib.oracle_scan_sum.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.c_int] + \
+            [ctypes.POINTER(ctypes.c_uint64)] * 4
         lib.oracle_sha256.restype = None
         lib.oracle_sha256.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         _lib = lib
@@ -104,6 +108,30 @@ def c_scan(msg, lo: int, hi: int, threads: int = 0):
     h, n = ctypes.c_uint64(), ctypes.c_uint64()
     _load().oracle_scan(m, len(m), lo, hi, threads, ctypes.byref(h), ctypes.byref(n))
     return int(h.value), int(n.value)
+
+
+def c_scan_sum(msg, lo: int, hi: int, threads: int = 0):
+    """c_scan plus the coverage checksum of hm_scan_checked:
+    ((hash, nonce), sum of every key mod 2^64, nonces hashed)."""
+    m = _b(msg)
+    if threads <= 0:
+        threads = min(16, os.cpu_count() or 1)
+    h, n, s, c = (ctypes.c_uint64() for _ in range(4))
+    _load().oracle_scan_sum(m, len(m), lo, hi, threads, ctypes.byref(h), ctypes.byref(n),
+                            ctypes.byref(s), ctypes.byref(c))
+    return (int(h.value), int(n.value)), int(s.value), int(c.value)
+
+
+def py_scan_sum(msg, lo: int, hi: int):
+    """py_scan plus the coverage checksum (independent hashlib restatement)."""
+    m = _b(msg)
+    result, index, total = MAXU64, 0, 0
+    for i in range(lo, hi + 1):
+        h = int.from_bytes(hashlib.sha256(m + b" " + str(i).encode()).digest()[:8], "big")
+        total += h
+        if h < result:
+            result, index = h, i
+    return (result, index), total & MAXU64, max(0, hi - lo + 1)
 
 
 def c_miner_eval(msg, lower: int, upper: int, threads: int = 0):

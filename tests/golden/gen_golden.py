@@ -33,13 +33,20 @@ def H(msg: bytes, n: int) -> int:
 
 
 def scan(args):
+    return scan_sum(args)[0]
+
+
+def scan_sum(args):
+    """(best, idx) plus the coverage checksum of hm_scan_checked:
+    the sum of every key mod 2^64 and the count of nonces."""
     msg, lo, hi = args
-    best, idx = MAX, 0
+    best, idx, total = MAX, 0, 0
     for i in range(lo, hi + 1):
         h = H(msg, i)
+        total += h
         if h < best:
             best, idx = h, i
-    return best, idx
+    return (best, idx), total & MAX, max(0, hi - lo + 1)
 
 
 def miner_eval(msg, lower, upper):
@@ -130,13 +137,13 @@ def main():
     for L in (0, 8, 44, 45, 55, 56, 63, 64, 119, 120):
         cases.append((f"len{L}", msg_of_len(L), 0, 300000))
     with Pool(min(8, os.cpu_count() or 1)) as pool:
-        res = pool.map(scan, [(m, lo, hi) for _, m, lo, hi in cases], chunksize=1)
+        res = pool.map(scan_sum, [(m, lo, hi) for _, m, lo, hi in cases], chunksize=1)
     sk = []
-    for (name, m, lo, hi), (h, n) in zip(cases, res):
+    for (name, m, lo, hi), ((h, n), sm, cnt) in zip(cases, res):
         sk.append({"name": name, "msg_hex": m.hex(), "lo": str(lo), "hi": str(hi),
-                   "hash": str(h), "nonce": str(n)})
+                   "hash": str(h), "nonce": str(n), "sum": str(sm), "count": str(cnt)})
     sk.append({"name": "empty-range", "msg_hex": b.hex(), "lo": "5", "hi": "4",
-               "hash": str(MAX), "nonce": "0"})
+               "hash": str(MAX), "nonce": "0", "sum": "0", "count": "0"})
     out["scan_kats"] = sk
 
     me = []

@@ -11,7 +11,8 @@ def test_exports_every_header_symbol():
     lib = _lib.load()
     syms = _lib.header_symbols()
     assert set(syms) >= {"hm_hash", "hm_open", "hm_scan", "hm_scan_stats", "hm_set_option",
-                         "hm_strerror", "hm_close", "hm_version"}
+                         "hm_strerror", "hm_close", "hm_version", "hm_scan_checked",
+                         "hm_scan_many", "hm_partition"}
     for s in syms:
         assert hasattr(lib, s), s
 
@@ -24,6 +25,7 @@ def test_library_is_gfx950_code_object():
 def test_version_and_strerror():
     lib = _lib.load()
     assert lib.hm_version() >> 16 == 1
+    assert lib.hm_version() & 0xFFFF >= 3  # 1.3: hm_scan_checked
     for rc in range(0, -7, -1):
         assert _lib.strerror(rc)
     assert _lib.strerror(-99) == "unknown error"
@@ -38,6 +40,7 @@ def test_hm_hash_matches_golden(golden):
 def test_null_args():
     lib = _lib.load()
     assert lib.hm_scan(None, b"x", 1, 0, 1, None) == _lib.HM_ERR_INVALID
+    assert lib.hm_scan_checked(None, b"x", 1, 0, 1, None, None, None) == _lib.HM_ERR_INVALID
     assert lib.hm_open(None, -1, None) == _lib.HM_ERR_INVALID
     assert lib.hm_set_option(None, 1, 1) == _lib.HM_ERR_INVALID
     lib.hm_close(None)

@@ -1,0 +1,166 @@
+"""Coverage checksums on the GPU: hm_scan_checked vs the oracle and vs itself.
+
+hm_scan_checked runs the checked variants of the production kernels (same
+planner, tiles, lane/loop layout, guided task split, launch chunking and
+multi-device shards) and returns, besides the (hash, nonce) minimum, the sum of
+every key mod 2^64 and the number of nonces hashed.  A nonce skipped, hashed
+twice or hashed over wrong bytes changes that pair, so these tests check that
+every nonce of a range is hashed exactly once and correctly:
+
+* against the golden fixtures (tests/golden/gen_golden.py, hashlib) and the C
+  oracle (oracle/hm_oracle.c, oracle_scan_sum) at sizes the CPU finishes in
+  seconds;
+* against tests/golden/large.json at the full BASELINE sizes (2^32 nonces of
+  configs[1] and configs[2], computed once by the 8-thread C oracle);
+* beyond any CPU rescan, through size-independent properties: the sums of
+  disjoint shards add up to the sum of their union, the counts are exact, and
+  the independent generic kernel gives the same triple.
+"""
+import json
+import os
+import random
+
+import pytest
+
+from distributed_bitcoinminer_amd import _lib
+
+pytestmark = pytest.mark.gpu
+MAX = (1 << 64) - 1
+M64 = MAX
+
+
+def _add(parts):
+    best = min(((h, n) for (h, n), _, _ in parts), default=(MAX, 0))
+    return best, sum(s for _, s, _ in parts) & M64, sum(c for _, _, c in parts)
+
+
+def _generic(ctx, m, lo, hi):
+    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+    try:
+        return ctx.scan_checked(m, lo, hi)
+    finally:
+        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+
+
+def test_checked_golden(ctx, golden):
+    n = 0
+    for case in golden["scan_kats"]:
+        if "sum" not in case:
+            continue
+        m = bytes.fromhex(case["msg_hex"])
+        lo, hi = int(case["lo"]), int(case["hi"])
+        exp = ((int(case["hash"]), int(case["nonce"])), int(case["sum"]), int(case["count"]))
+        assert ctx.scan_checked(m, lo, hi) == exp, (case["name"], lo, hi)
+        n += 1
+    assert n >= 390
+
+
+def test_checked_min_equals_scan(ctx):
+    for m, lo, hi in [(b"bradfitz", 0, 10**7), (b"x" * 57, 10**9 - 10**6, 10**9 + 10**6),
+                      (b"bradfitz", MAX - 10**6, MAX)]:
+        (best, _, cnt) = ctx.scan_checked(m, lo, hi)
+        assert best == ctx.scan(m, lo, hi) and cnt == hi - lo + 1
+
+
+def test_checked_layout_sweep_vs_oracle(ctx, oracle_mod):
+    """Every message length 0..130 x every digit count, both ends of each digit
+    segment (partial tiles, surplus lanes, digit-count changes)."""
+    rng = random.Random(5)
+    for L in range(0, 131):
+        m = bytes(rng.randrange(256) for _ in range(L))
+        for d in range(1, 21):
+            dlo = 0 if d == 1 else 10**(d - 1)
+            dhi = min(10**d - 1, MAX)
+            for lo, hi in ((dlo, min(dhi, dlo + 500)), (max(dlo, dhi - 400), min(MAX, dhi + 200))):
+                assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, d, lo, hi)
+
+
+def test_checked_whole_tiles_vs_generic(ctx):
+    """Whole tiles of every fast layout (tiled / chained, W1, straddle, trailer,
+    V) against the generic kernel's checked scan, including ranges large
+    enough to use both whole and split (guided) tasks."""
+    rng = random.Random(78)
+    seen = set()
+    for L in range(0, 131):
+        m = bytes(rng.randrange(32, 127) for _ in range(L))
+        for d in (7, 8, 10, 12, 16, 20):
+            dlo, dhi = 10**(d - 1), min(10**d - 1, MAX)
+            seg = _lib.debug_plan(m, dlo, dhi)[0]
+            if seg["kind"] == _lib.HM_KIND_GENERIC:
+                continue
+            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"])
+            if key in seen:
+                continue
+            seen.add(key)
+            span = min(3 * 10**seg["V"] + 4321, 6 * 10**7, (dhi - dlo) // 2)
+            lo = rng.randrange(dlo, dhi - span)
+            fast = ctx.scan_checked(m, lo, lo + span)
+            assert fast == _generic(ctx, m, lo, lo + span), (L, d, key)
+            assert fast[2] == span + 1
+    assert len(seen) >= 40, len(seen)
+
+
+def test_checked_guided_split_boundaries(ctx):
+    """bradfitz d=10: units of 6400 nonces; around one unit per wave of the
+    grid the launch switches from whole units to tenths.  Ranges below, at and
+    above that size, cut at arbitrary points, add up exactly."""
+    base = 3_000_000_000 + 12_345
+    whole = ctx.scan_checked(b"bradfitz", base, base + 80_000_000)
+    cuts = [base, base + 1, base + 6399, base + 20_000_000, base + 33_000_001,
+            base + 64_000_000, base + 80_000_001]
+    parts = [ctx.scan_checked(b"bradfitz", a, b - 1) for a, b in zip(cuts, cuts[1:])]
+    assert _add(parts) == whole
+    assert whole == _generic(ctx, b"bradfitz", base, base + 80_000_000)
+
+
+def _large():
+    with open(os.path.join(os.path.dirname(__file__), "golden", "large.json")) as f:
+        return [c for c in json.load(f) if "sum" in c]
+
+
+@pytest.mark.parametrize("case", _large(), ids=lambda c: c["name"])
+def test_checked_full_size_pinned(ctx, case):
+    """BASELINE configs[1] and configs[2] at full size (2^32 nonces): minimum,
+    sum of all 2^32 keys and count equal the C oracle's (tests/golden/large.json);
+    uneven shards across digit and launch boundaries add up to the same."""
+    m, lo, hi = bytes.fromhex(case["msg_hex"]), int(case["lo"]), int(case["hi"])
+    exp = ((int(case["hash"]), int(case["nonce"])), int(case["sum"]), int(case["count"]))
+    assert ctx.scan_checked(m, lo, hi) == exp
+    cuts = [lo, 99_999_999, 10**9 - 3, 10**9 + 11, 2_147_483_648, 3_999_999_999, hi + 1]
+    assert _add([ctx.scan_checked(m, a, b - 1) for a, b in zip(cuts, cuts[1:])]) == exp
+
+
+def test_checked_beyond_cpu(ctx):
+    """1.2e11 nonces of bradfitz at d=12 (two chunked launches of 2^20 tiles):
+    no CPU can rescan it, so the count must be exact, shards split at the launch
+    boundary and elsewhere must add up, and a window around the boundary must
+    match the generic kernel."""
+    lo, hi = 10**11, 10**11 + 120_000_000_000
+    whole = ctx.scan_checked(b"bradfitz", lo, hi)
+    assert whole[2] == hi - lo + 1
+    boundary = (lo // 10**5 + (1 << 20)) * 10**5
+    cuts = [lo, lo + 7_777_777_777, boundary - 3, boundary + 5, hi + 1]
+    assert _add([ctx.scan_checked(b"bradfitz", a, b - 1) for a, b in zip(cuts, cuts[1:])]) == whole
+    w_lo, w_hi = boundary - 20_000_000, boundary + 20_000_000
+    assert ctx.scan_checked(b"bradfitz", w_lo, w_hi) == _generic(ctx, b"bradfitz", w_lo, w_hi)
+    assert _lib.host_hash(b"bradfitz", whole[0][1]) == whole[0][0]
+
+
+def test_checked_multi_device_and_streams(oracle_mod):
+    """Shards over 2 and 3 'devices' (device 0 opened repeatedly) and 4 streams
+    cover the range exactly once: same triple as one device and the oracle."""
+    cases = [(b"a" * 45, 10**9 - 900_000, 10**9 + 300_000),
+             (b"jonny greenwood", 10**8 - 2_000_000, 10**8 + 1_000_000),
+             (b"bradfitz", MAX - 300_000, MAX)]
+    exp = [oracle_mod.c_scan_sum(m, lo, hi) for m, lo, hi in cases]
+    for devs, streams in (([0], 1), ([0], 4), ([0, 0], 1), ([0, 0, 0], 4)):
+        with _lib.Context(devs) as c:
+            c.set_option(_lib.HM_OPT_STREAMS, streams)
+            for (m, lo, hi), e in zip(cases, exp):
+                assert c.scan_checked(m, lo, hi) == e, (devs, streams, m, lo, hi)
+
+
+def test_checked_empty_and_edges(ctx):
+    assert ctx.scan_checked(b"bradfitz", 5, 4) == ((MAX, 0), 0, 0)
+    assert ctx.scan_checked(b"bradfitz", MAX, MAX) == ((_lib.host_hash(b"bradfitz", MAX), MAX),
+                                                        _lib.host_hash(b"bradfitz", MAX), 1)

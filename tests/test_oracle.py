@@ -37,6 +37,17 @@ def test_scan_kats(oracle_mod, golden):
         exp = (int(k["hash"]), int(k["nonce"]))
         assert oracle_mod.c_scan(m, lo, hi, threads=4) == exp, (k["name"], lo, hi)
         assert oracle_mod.c_scan(m, lo, hi, threads=1) == exp
+        if "sum" in k:  # coverage checksum of hm_scan_checked
+            assert oracle_mod.c_scan_sum(m, lo, hi, threads=3) == \
+                (exp, int(k["sum"]), int(k["count"])), (k["name"], lo, hi)
+
+
+def test_scan_sum_thread_invariance_and_python(oracle_mod):
+    for m, lo, hi in [(b"bradfitz", 0, 2000), (b"q" * 56, 99_000, 101_000), (b"", MAX - 40, MAX),
+                      (b"x", 5, 4)]:
+        exp = oracle_mod.py_scan_sum(m, lo, hi)
+        for t in (1, 2, 7):
+            assert oracle_mod.c_scan_sum(m, lo, hi, threads=t) == exp, (m, lo, hi, t)
 
 
 def test_config1_oracle(oracle_mod):
