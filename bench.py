@@ -20,9 +20,11 @@ roofline: INT32 VALU, SURVEY §8(d): algorithmic work = 1552 lane-ops per
 SHA-256 compression x C compressions per nonce; achieved = that work in the
 dominant scan launch / its HIP-event duration (measured live, on the stream
 the kernel runs on); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
-cpu_baseline: the C restatement of the reference loop (oracle/hm_oracle.c,
-format + SHA-256 from the IV per nonce, strict <), 1 thread = one reference
-miner, on a bounded sample of the same message.
+cpu_baseline: the reference miner fleet restated on the host -- one thread
+per core of this process's CPU share (<= 16), each a sequential miner over
+its own chunk, running the C restatement of the reference loop
+(oracle/hm_oracle.c: format + SHA-256 from the IV per nonce, strict <) on a
+bounded sample of the same message; one miner alone is reported beside it.
 """
 from __future__ import annotations
 
@@ -71,24 +73,52 @@ def profiled(kernel: str):
             return k["hbm_bytes_per_launch"], k["f_eff_ghz_largest_dispatch"], \
                 os.path.relpath(path, ROOT)
     return None, None, None
+
+
 OPS_PER_COMPRESSION = 1552
 PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T INT32 lane-ops/s
 CPU_SAMPLE = 50_000_000              # nonces for the 1-thread CPU baseline (~12 s on the GPU box host)
+CPU_FLEET_PER_THREAD = 40_000_000    # nonces per thread of the fleet sample (~9 s)
+
+
+def _cpu_share() -> int:
+    """Host threads this process may use: its affinity set, capped at the GPU
+    box's per-GPU share (16; OMP_NUM_THREADS is set to it there)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
 
 
 def cpu_baseline(msg: bytes, name: str):
+    """The reference miner fleet restated on the host: one
+    sequential miner per core on disjoint equal chunks (oracle/hm_oracle.c:
+    Sprintf-style format + SHA-256 from the IV per nonce, strict <), plus one
+    miner alone."""
+    import platform
     from oracle import oracle
     oracle.build()
     oracle.c_scan(msg, 0, 100_000, threads=1)  # warm
-    n = CPU_SAMPLE if len(msg) + 21 <= 55 else CPU_SAMPLE // 3  # 1 vs 3 compressions per nonce
+    scale = 1 if len(msg) + 21 <= 55 else 3  # 1 vs 3 compressions per nonce
+    n1 = CPU_SAMPLE // scale
     t = time.perf_counter()
-    oracle.c_scan(msg, 0, n - 1, threads=1)
-    dt = time.perf_counter() - t
-    return {"value": n / dt / 1e9, "unit": "GH/s", "cores": 1, "kind": "port",
-            "sample": f"{name} nonces [0, {n}) with oracle/hm_oracle.c "
-                      f"(Sprintf-style format + SHA-256 from the IV per nonce, strict <), "
-                      f"1 thread; {dt:.2f} s",
-            "mhs": n / dt / 1e6}
+    oracle.c_scan(msg, 0, n1 - 1, threads=1)
+    d1 = time.perf_counter() - t
+    cores = _cpu_share()
+    nN = CPU_FLEET_PER_THREAD // scale * cores
+    t = time.perf_counter()
+    oracle.c_scan(msg, 0, nN - 1, threads=cores)
+    dN = time.perf_counter() - t
+    cpu = next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                if l.startswith("model name")), platform.processor() or "?")
+    return {"value": nN / dN / 1e9, "unit": "GH/s", "cores": cores, "kind": "port",
+            "sample": f"{name}: a fleet of {cores} CPU miners (one thread each, disjoint equal "
+                      f"chunks of [0, {nN})) running oracle/hm_oracle.c, the C restatement of "
+                      f"the reference loop (Sprintf-style format + SHA-256 from the IV per "
+                      f"nonce, strict <); {dN:.2f} s on {cpu}",
+            "single_miner": {"value": n1 / d1 / 1e9, "unit": "GH/s", "cores": 1,
+                             "sample": f"[0, {n1}) on 1 thread, {d1:.2f} s"}}
 
 
 def main():
@@ -225,7 +255,7 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(msg, args.workload)
-            line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind", "sample")}
+            line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist is not None:

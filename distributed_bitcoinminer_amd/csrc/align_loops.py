@@ -1,0 +1,287 @@
+#!/usr/bin/env python3
+"""Instruction placement pass for the scan kernels' hot loops (build step).
+
+gfx950 issues a long VALU stream measurably faster when its 8-byte (VOP3)
+instructions start at addresses = 4 mod 8: the same hm_tiled_kernel inner
+loop ran at 34.6 GH/s with 75 % of its 8-byte VALU instructions at 4 mod 8
+and at 32.9 GH/s with 24 % (one 4-byte `s_nop` apart; same box, one process;
+DESIGN.md §4 "Instruction placement").  hipcc leaves this to chance, so any
+edit of the kernels could move a kernel by +-5 %.  MI355X_MICROARCH.md
+("Code-placement sensitivity of hand-written streams") reports the same
+effect for hand-written asm.
+
+This pass makes the placement deliberate.  For every kernel whose innermost
+loop holds >= MIN_LOOP instructions it walks the loop in address order and,
+whenever an 8-byte VALU instruction would start at 0 mod 8, shifts it by 4:
+by re-encoding the nearest preceding 4-byte VALU instruction of a full-rate
+kind (v_add_u32, v_xor_b32, ... e32 -> e64: the same operation and issue
+cost in 8 bytes), or, when there is none since the previous 8-byte VALU
+instruction, by inserting `s_nop 0` in front of it.  Nothing else changes:
+the same instructions, registers, order and waits.
+
+usage: align_loops.py <in.s> <out.s> [--report] [--phase 4|0] [--no-nop]
+(--phase 0 and --no-nop are for placement experiments only.)
+The input is `hipcc --cuda-device-only -S` output for gfx950; the output is
+assembled into the code object that api.cpp loads (see the Makefile).  The
+pass re-assembles its output and fails unless every 8-byte VALU instruction
+of every hot loop starts at 4 mod 8.
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+MIN_LOOP = 500
+LATCH_BYTES = 64  # a latch block placed in front of the loop header
+PROMOTE = {"v_add_u32_e32": "v_add_u32_e64", "v_xor_b32_e32": "v_xor_b32_e64",
+           "v_or_b32_e32": "v_or_b32_e64", "v_and_b32_e32": "v_and_b32_e64",
+           "v_sub_u32_e32": "v_sub_u32_e64", "v_mov_b32_e32": "v_mov_b32_e64"}
+INST = re.compile(r"^\s+([a-z][a-z0-9_]*)(\s|$)")
+FUNC = re.compile(r"^(_Z\w+):")
+DIS = re.compile(r"^\s+(\S+)\s*(.*?)\s*//\s*([0-9A-F]+):((?:\s[0-9A-F]{8})+)"
+                 r"(?:\s*<(\S+)\+0x([0-9a-f]+)>)?")
+
+
+def assemble(src_path, obj_path):
+    subprocess.run([f"{LLVM}/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
+                    "-mcpu=gfx950", "-c", src_path, "-o", obj_path], check=True)
+
+
+def disassemble(obj_path):
+    """symbol -> [(addr, size, opcode, branch_target_or_None)]"""
+    out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--mcpu=gfx950", obj_path],
+                         capture_output=True, text=True, check=True).stdout
+    funcs, base, cur = {}, {}, None
+    for line in out.split("\n"):
+        m = re.match(r"^([0-9a-f]+) <(\S+)>:", line)
+        if m:
+            cur = m.group(2)
+            base[cur] = int(m.group(1), 16)
+            funcs[cur] = []
+            continue
+        m = DIS.match(line)
+        if m and cur:
+            tgt = None
+            if m.group(5) and m.group(5) in base:
+                tgt = base[m.group(5)] + int(m.group(6), 16)
+            funcs[cur].append((int(m.group(3), 16), 4 * len(m.group(4).split()), m.group(1), tgt))
+    return funcs
+
+
+def source_insts(lines):
+    """symbol -> [line index of each instruction, in order]"""
+    out, cur = {}, None
+    for i, line in enumerate(lines):
+        m = FUNC.match(line)
+        if m:
+            cur = m.group(1)
+            out[cur] = []
+            continue
+        if line.startswith(".Lfunc_end"):
+            cur = None
+            continue
+        if cur and INST.match(line):
+            out[cur].append(i)
+    return out
+
+
+def inner_headers(lines, idx):
+    """Instruction indices (into idx) that open an innermost loop, from the
+    compiler's '; => This Inner Loop Header' annotations."""
+    pos = {line_no: k for k, line_no in enumerate(idx)}
+    heads = []
+    for k, line_no in enumerate(idx):
+        j = line_no - 1
+        while j >= 0 and lines[j].lstrip().startswith(";"):
+            if "Inner Loop Header" in lines[j]:
+                heads.append(k)
+                break
+            j -= 1
+    return heads
+
+
+def hot_loop(insts, heads):
+    """(first, last) instruction index of the innermost loop with the most
+    instructions (>= MIN_LOOP), from its first block to its back-edge.  hipcc
+    may place the loop's latch block just in front of the header; the back-edge
+    then targets the latch.  Rare-path blocks placed after the back-edge are
+    excluded."""
+    best = None
+    addr_index = {x[0]: i for i, x in enumerate(insts)}
+    for k in heads:
+        if k >= len(insts):
+            continue
+        head = insts[k][0]
+        ends = [(i, x[3]) for i, x in enumerate(insts)
+                if i > k and x[3] is not None and head - LATCH_BYTES <= x[3] <= head]
+        if not ends:
+            continue
+        end, target = max(ends)
+        first = addr_index[target]
+        if end - first + 1 >= MIN_LOOP and (best is None or end - first > best[1] - best[0]):
+            best = (first, end)
+    return best
+
+
+PHASE = 4  # target start address mod 8 of 8-byte VALU instructions
+NO_NOP = False
+
+
+def stats(insts, lo, hi):
+    big = [x for x in insts[lo:hi + 1] if x[1] == 8 and x[2].startswith("v_")]
+    return sum(1 for x in big if x[0] % 8 == PHASE), len(big)
+
+
+REG = re.compile(r"\b([vs])(\d+)\b|\b([vs])\[(\d+):(\d+)\]|\b(vcc|exec|scc|m0)\b")
+# 4-byte VALU instructions that may trade places with the next 8-byte one:
+# plain two-operand ALU ops without implicit operands
+MOVABLE = set(PROMOTE) | {"v_lshrrev_b32_e32", "v_lshlrev_b32_e32", "v_ashrrev_i32_e32"}
+# 8-byte VALU instructions they may be moved across: plain ALU, no lane
+# crossing, no implicit VCC/EXEC
+PLAIN8 = re.compile(r"^v_(alignbit|alignbyte|add3|bitop3|xad|lshl_add|lshl_or|and_or|or3|"
+                    r"bfi|perm|add_u32_e64|xor_b32_e64|sub_u32_e64|lshl_add_u64)")
+
+
+def regs(operands):
+    out = set()
+    for m in REG.finditer(operands):
+        if m.group(1):
+            out.add(m.group(1) + m.group(2))
+        elif m.group(3):
+            out.update(f"{m.group(3)}{r}" for r in range(int(m.group(4)), int(m.group(5)) + 1))
+        else:
+            out.add(m.group(6))
+    return out
+
+
+def rw(text):
+    """(written, read) register sets of one VALU instruction line."""
+    ops = text.split(None, 1)[1] if len(text.split(None, 1)) > 1 else ""
+    ops = ops.split(";")[0].split("//")[0]
+    parts = [p.strip() for p in ops.split(",")]
+    return regs(parts[0]), regs(",".join(parts[1:]))
+
+
+def plan_fixes(insts, lo, hi, text):
+    """Make every 8-byte VALU instruction of insts[lo..hi] start at 4 mod 8.
+
+    Returns (order, promote, nops): the new order of the loop's instruction
+    indices, the indices re-encoded from 4 to 8 bytes, and the indices to be
+    prefixed with `s_nop 0`.  Between two consecutive 8-byte VALU
+    instructions an odd number of 4-byte instructions flips the parity; each
+    such gap gets one fix, cheapest first: re-encode a full-rate 4-byte VALU
+    op of the gap as e64; move the gap's last 4-byte VALU op behind the next
+    8-byte instruction when the two are independent; else insert s_nop."""
+    order = list(range(lo, hi + 1))
+    promote, nops = set(), set()
+    addr = insts[lo][0]
+    pos = 0
+    gap = []  # positions (in order) of 4-byte instructions since the last 8-byte VALU
+    while pos < len(order):
+        k = order[pos]
+        _, size, op, _ = insts[k]
+        if size == 8 and op.startswith("v_"):
+            if addr % 8 != PHASE:
+                prom = [p for p in gap if insts[order[p]][2] in PROMOTE]
+                last = gap[-1] if gap else None
+                if prom:
+                    promote.add(order[prom[-1]])
+                    addr += 4
+                elif (last == pos - 1 and insts[order[last]][2] in MOVABLE
+                      and PLAIN8.match(op)):
+                    lw, lr = rw(text[order[last]])
+                    ew, er = rw(text[k])
+                    if not (lw & (ew | er)) and not (ew & lr):
+                        # the 8-byte op now starts where the 4-byte one did
+                        # (addr - 4, = 4 mod 8); the 4-byte op follows it and
+                        # opens the next gap
+                        order[last], order[pos] = order[pos], order[last]
+                        addr += 4 + 4
+                        gap = [pos]
+                        pos += 1
+                        continue
+                    if not NO_NOP:
+                        nops.add(k)
+                        addr += 4
+                elif not NO_NOP:
+                    nops.add(k)
+                    addr += 4
+            gap = []
+        elif size == 4:
+            gap.append(pos)
+        addr += size
+        pos += 1
+    return order, promote, nops
+
+
+def main():
+    global PHASE, NO_NOP
+    src, dst = sys.argv[1], sys.argv[2]
+    report = "--report" in sys.argv
+    if "--phase" in sys.argv:
+        PHASE = int(sys.argv[sys.argv.index("--phase") + 1])
+    NO_NOP = "--no-nop" in sys.argv
+    with open(src) as f:
+        lines = f.read().split("\n")
+    with tempfile.TemporaryDirectory() as td:
+        obj = os.path.join(td, "in.o")
+        assemble(src, obj)
+        funcs = disassemble(obj)
+        where = source_insts(lines)
+        edits = {}  # line index -> replacement text
+        loops = {}
+        for sym, insts in funcs.items():
+            if sym not in where:
+                continue
+            idx = where[sym]
+            # the disassembly may list the inter-function alignment padding too
+            if len(idx) > len(insts):
+                raise SystemExit(f"{sym}: {len(idx)} source vs {len(insts)} encoded instructions")
+            loop = hot_loop(insts, inner_headers(lines, idx))
+            if loop is None:
+                continue
+            loops[sym] = loop
+            for k, (_, _, op, _) in enumerate(insts[:len(idx)]):
+                if INST.match(lines[idx[k]]).group(1) != op:
+                    raise SystemExit(f"{sym}: instruction {k} is {op} in the object, "
+                                     f"'{lines[idx[k]].strip()}' in the source")
+            lo, hi = loop
+            text = {k: lines[idx[k]] for k in range(lo, hi + 1)}
+            order, promote, nops = plan_fixes(insts, lo, hi, text)
+            new = {}
+            for k in range(lo, hi + 1):
+                t = text[k]
+                if k in promote:
+                    t = t.replace(insts[k][2], PROMOTE[insts[k][2]], 1)
+                if k in nops:
+                    t = "\ts_nop 0\n" + t
+                new[k] = t
+            for slot, k in zip(range(lo, hi + 1), order):
+                edits[idx[slot]] = new[k]
+            if report:
+                good, n = stats(insts, lo, hi)
+                moved = sum(1 for a, b in zip(range(lo, hi + 1), order) if a != b) // 2
+                print(f"{sym[:64]:64s} loop {hi - lo + 1:5d} insts: {good:4d}/{n} 8-B VALU at "
+                      f"4 mod 8 -> re-encode {len(promote)}, move {moved}, s_nop {len(nops)}")
+        with open(dst, "w") as f:
+            f.write("\n".join(edits.get(i, l) for i, l in enumerate(lines)))
+        obj2 = os.path.join(td, "out.o")
+        assemble(dst, obj2)
+        with open(dst) as f:
+            lines2 = f.read().split("\n")
+        where2 = source_insts(lines2)
+        for sym, insts in disassemble(obj2).items():
+            if sym not in loops:
+                continue
+            loop = hot_loop(insts, inner_headers(lines2, where2[sym]))
+            good, n = stats(insts, *loop)
+            if report:
+                print(f"  after: {sym[:60]:60s} {good}/{n}")
+            if good != n and not NO_NOP:
+                raise SystemExit(f"{sym}: {n - good} 8-byte VALU instructions not at {PHASE} mod 8")
+
+
+if __name__ == "__main__":
+    main()

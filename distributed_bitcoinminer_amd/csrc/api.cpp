@@ -7,11 +7,15 @@
 //   host:  plan_message (midstate) -> plan_range (digit segments, layouts)
 //   GPU :  per segment, on one of kStreams HIP streams
 //            [tiled]   hm_tile_plan_kernel -> counter reset -> hm_tiled_kernel
+//            [chained] hm_kw_table_kernel, hm_tile_plan_kernel -> hm_chained_kernel
 //            [generic] hm_generic_kernel
 //          -> hm_fold_kernel (per-wave candidates -> per-stream best)
 //          -> join streams -> hm_fold_kernel (stream bests -> 16-B result)
 //   multi-device: contiguous shards, then either a host merge of the 16-B
 //          results or an RCCL all-gather of them (HM_OPT_MERGE_RCCL).
+//   The scan kernels come from their own code object (scan_kernels.hip ->
+//   align_loops.py -> hipminer_scan.hsaco, embedded by scan_blob.S), loaded
+//   per device with hipModuleLoadData and launched with hipModuleLaunchKernel.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <stdio.h>
@@ -20,6 +24,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
@@ -30,6 +35,9 @@
 #include "plan.hpp"
 
 using namespace hm;
+
+// The scan kernels' code object (scan_blob.S .incbin of hipminer_scan.hsaco).
+extern "C" const unsigned char hm_scan_code_object[];
 
 namespace {
 
@@ -68,6 +76,9 @@ struct Device {
     size_t evnext = 0;
     std::vector<Launch> launches;
     ncclComm_t comm = nullptr;
+    hipModule_t mod = nullptr;  // scan kernels (hipminer_scan.hsaco)
+    struct Fn { std::string sym; hipFunction_t fn; int blocks_per_cu; };
+    std::deque<Fn> fns;         // resolved on first use (stable addresses)
 };
 
 bool debug_on() {
@@ -118,6 +129,7 @@ int device_init(Device& dv, int ordinal) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, ordinal));
     dv.cus = prop.multiProcessorCount;
+    HIPCHK(hipModuleLoadData(&dv.mod, hm_scan_code_object));
     for (int s = 0; s < kStreams; ++s) {
         HIPCHK(hipStreamCreateWithFlags(&dv.stream[s], hipStreamNonBlocking));
         HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
@@ -151,12 +163,56 @@ void device_free(Device& dv) {
         if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
     }
     for (hipEvent_t e : dv.evpool) (void)hipEventDestroy(e);
+    if (dv.mod) (void)hipModuleUnload(dv.mod);
+    dv.fns.clear();
     if (dv.best) (void)hipFree(dv.best);
     if (dv.acc) (void)hipFree(dv.acc);
     if (dv.result) (void)hipFree(dv.result);
     if (dv.gathered) (void)hipFree(dv.gathered);
     if (dv.host_out) (void)hipHostFree(dv.host_out);
     dv.ordinal = -1;
+}
+
+// Mangled names of the scan kernels in hipminer_scan.hsaco (scan_kernels.hip).
+std::string tiled_symbol(const SegPlan& s, bool csum) {
+    char b[128];
+    snprintf(b, sizeof b, "_ZN2hm%s_kernelILi%dELb%dELb%dEEEvNS_9TiledArgsE",
+             csum ? "20hm_tiled_csum" : "15hm_tiled", s.W1, s.straddle ? 1 : 0,
+             s.trailer ? 1 : 0);
+    return b;
+}
+const char* chained_symbol(bool csum) {
+    return csum ? "_ZN2hm22hm_chained_csum_kernelENS_11ChainedArgsE"
+                : "_ZN2hm17hm_chained_kernelENS_11ChainedArgsE";
+}
+const char* generic_symbol(bool csum) {
+    return csum ? "_ZN2hm22hm_generic_csum_kernelENS_11GenericArgsE"
+                : "_ZN2hm17hm_generic_kernelENS_11GenericArgsE";
+}
+
+// Resolve a scan kernel of dv's module (cached with its occupancy).
+int scan_fn(Device& dv, const std::string& sym, const Device::Fn** out) {
+    for (const auto& f : dv.fns)
+        if (f.sym == sym) { *out = &f; return HM_OK; }
+    Device::Fn f{sym, nullptr, 0};
+    HIPCHK(hipModuleGetFunction(&f.fn, dv.mod, sym.c_str()));
+    HIPCHK(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&f.blocks_per_cu, f.fn, kBlock, 0));
+    dv.fns.push_back(f);
+    *out = &dv.fns.back();
+    return HM_OK;
+}
+
+// Launch a scan kernel with its argument block (the kernel's only, by-value
+// parameter) on `grid` workgroups of kBlock threads.
+template <typename Args>
+int launch_scan(const Device::Fn& f, const Args& args, int grid, hipStream_t st) {
+    if (grid < 1 || (uint32_t)grid * (kBlock / kWaveSize) > kMaxCandWaves)
+        return hip_fail(hipErrorInvalidValue, "scan grid");
+    size_t size = sizeof(Args);
+    void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, const_cast<Args*>(&args),
+                   HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+    HIPCHK(hipModuleLaunchKernel(f.fn, (unsigned)grid, 1, 1, kBlock, 1, 1, 0, st, nullptr, cfg));
+    return HM_OK;
 }
 
 uint32_t count_compressions(const SegPlan& s) {
@@ -232,10 +288,13 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.tch = s.tch;
         ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
         ca.q = s.q;
-        const int grid = persistent_grid(ctx, dv, chained_blocks_per_cu(), nunits);
+        const Device::Fn* fn = nullptr;
+        int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
+        if (rc) return rc;
+        const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
         ca.ntasks = guided_tasks(nunits, grid, &ca.nbig);
         Launch L;
-        int rc = next_event(dv, &L.start);
+        rc = next_event(dv, &L.start);
         if (rc) return rc;
         rc = next_event(dv, &L.stop);
         if (rc) return rc;
@@ -245,7 +304,8 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         L.grid = grid;
         L.compressions = count_compressions(s);
         HIPCHK(hipEventRecord(L.start, st));
-        HIPCHK(launch_chained(ca, grid, st, ctx->csum));
+        rc = launch_scan(*fn, ca, grid, st);
+        if (rc) return rc;
         HIPCHK(hipEventRecord(L.stop, st));
         HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si,
                            st));
@@ -304,11 +364,13 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.loop_shift = s.loop_shift;
             memcpy(ta.trailer_kw, kw, sizeof kw);
             tiled_loop_sigma0(s, ta.s0_loop);
-            const int grid = persistent_grid(
-                ctx, dv, tiled_blocks_per_cu(s.W1, s.straddle, s.trailer), nunits);
+            const Device::Fn* fn = nullptr;
+            int rc = scan_fn(dv, tiled_symbol(s, ctx->csum), &fn);
+            if (rc) return rc;
+            const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
             ta.ntasks = guided_tasks(nunits, grid, &ta.nbig);
             Launch L;
-            int rc = next_event(dv, &L.start);
+            rc = next_event(dv, &L.start);
             if (rc) return rc;
             rc = next_event(dv, &L.stop);
             if (rc) return rc;
@@ -318,7 +380,8 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             L.grid = grid;
             L.compressions = count_compressions(s);
             HIPCHK(hipEventRecord(L.start, st));
-            HIPCHK(launch_tiled(ta, s.W1, s.straddle, s.trailer, grid, st, ctx->csum));
+            rc = launch_scan(*fn, ta, grid, st);
+            if (rc) return rc;
             HIPCHK(hipEventRecord(L.stop, st));
             HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize),
                                best + 2 * si, st));
@@ -346,8 +409,11 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     const uint64_t need = ga.count_m1 / kBlock + 1;
     const uint64_t cap = (uint64_t)(kMaxCandWaves / (kBlock / kWaveSize));
     const int grid = (int)std::min<uint64_t>(need, std::min<uint64_t>(cap, (uint64_t)dv.cus * 8));
+    const Device::Fn* fn = nullptr;
+    int rc = scan_fn(dv, generic_symbol(ctx->csum), &fn);
+    if (rc) return rc;
     Launch L;
-    int rc = next_event(dv, &L.start);
+    rc = next_event(dv, &L.start);
     if (rc) return rc;
     rc = next_event(dv, &L.stop);
     if (rc) return rc;
@@ -357,7 +423,8 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     L.grid = grid;
     L.compressions = count_compressions(s);
     HIPCHK(hipEventRecord(L.start, st));
-    HIPCHK(launch_generic(ga, grid, st, ctx->csum));
+    rc = launch_scan(*fn, ga, grid, st);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(L.stop, st));
     HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si, st));
     if (ctx->csum)

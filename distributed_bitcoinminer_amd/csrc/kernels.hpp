@@ -101,23 +101,14 @@ struct GenericArgs {
     uint32_t mid[8];
 };
 
-// Launchers (return hipError_t of the launch).
+// Launchers of the auxiliary kernels (kernels.hip; return hipError_t of the
+// launch).  The scan kernels (scan_kernels.hip: hm_tiled_kernel<W1,
+// STRADDLE, TRAILER>, hm_chained_kernel, hm_generic_kernel and their
+// hm_*_csum_kernel checked variants) live in their own code object and are
+// launched by api.cpp through hipModuleLaunchKernel.
 hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s);
-// W1 in [1, 15], straddle: loop tens digit in W[W1-1], trailer: constant
-// final block after the digit block.  Returns hipErrorInvalidValue for an
-// unsupported combination.
-//
-// csum: the checked variant (hm_*_csum_kernel) of the same kernel.  It also
-// accumulates, per wave, the wrapping sum of the keys and the count of the
-// in-range nonces it hashed into a.sums -- the coverage checksum of
-// hm_scan_checked (every nonce of [lo, hi] hashed exactly once).
-hipError_t launch_tiled(const TiledArgs& a, int W1, bool straddle, bool trailer, int grid,
-                        hipStream_t s, bool csum = false);
-hipError_t launch_generic(const GenericArgs& a, int grid, hipStream_t s, bool csum = false);
-hipError_t launch_chained(const ChainedArgs& a, int grid, hipStream_t s, bool csum = false);
 // acc[0] += sum of sums[2i], acc[1] += sum of sums[2i+1] for i < n (wrapping).
 hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipStream_t s);
-int chained_blocks_per_cu();
 // K+W table of the final block for loop values t in [0, 10^f).
 hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s);
 // Fold n (key, nonce) pairs (pair i at cand + 2*i*stride) plus *best into
@@ -125,7 +116,5 @@ hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipSt
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
                        uint32_t stride = 1);
 hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);
-// Occupancy-derived persistent grid (workgroups) for the tiled kernel.
-int tiled_blocks_per_cu(int W1, bool straddle, bool trailer);
 
 }  // namespace hm

@@ -1,0 +1,176 @@
+// sha_device.hpp -- device-side building blocks of the scan kernels (gfx950):
+// SHA-256 rounds specialised by which message words vary, wave reductions.
+//
+// The reference computes SHA-256 through Go's crypto/sha256 inside
+// bitcoin.Hash (cmu440/bitcoin/hash.go:14-16); the scan loop is
+// cmu440/bitcoin/miner/miner.go:63-76.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "kernels.hpp"
+#include "sha256_defs.hpp"
+
+namespace hm {
+
+#define DEV __device__ __forceinline__
+
+DEV uint32_t rotr(uint32_t x, uint32_t n) { return __builtin_rotateright32(x, n); }
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one VALU op (LUT
+// index 4*src0 + 2*src1 + src2; 0x96 = three-way XOR).  hipcc forms bitop3
+// for Ch/Maj but not for XOR chains, so the Sigma functions use it directly.
+// Non-volatile asm: the compiler may still hoist/CSE it.
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// V = the value varies across lanes (VGPR): use bitop3; otherwise plain C so
+// the compiler folds wave-uniform work onto the scalar unit / hoists it.
+template <bool V> DEV uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    if constexpr (V) return xor3(a, b, c);
+    else return a ^ b ^ c;
+}
+template <bool V = true> DEV uint32_t bsig0(uint32_t x) { return x3<V>(rotr(x, 2), rotr(x, 13), rotr(x, 22)); }
+template <bool V = true> DEV uint32_t bsig1(uint32_t x) { return x3<V>(rotr(x, 6), rotr(x, 11), rotr(x, 25)); }
+template <bool V = true> DEV uint32_t ssig0(uint32_t x) { return x3<V>(rotr(x, 7), rotr(x, 18), x >> 3); }
+template <bool V = true> DEV uint32_t ssig1(uint32_t x) { return x3<V>(rotr(x, 17), rotr(x, 19), x >> 10); }
+// Ch = bfi(e, f, g); Maj = bfi(a ^ b, c, b) -- hipcc emits v_bitop3 for both
+DEV uint32_t ch(uint32_t e, uint32_t f, uint32_t g) { return ((f ^ g) & e) ^ g; }
+DEV uint32_t maj(uint32_t a, uint32_t b, uint32_t c) { return ((b ^ c) & (a ^ b)) ^ b; }
+
+DEV uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+DEV uint64_t uni64(uint64_t x) {
+    return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
+// Compile-time variability of the 64 schedule words given the mask VM of
+// message words that vary across lanes (bit i = W[i]).
+constexpr uint64_t sched_vary(uint32_t vm) {
+    uint64_t m = vm;
+    for (int t = 16; t < 64; ++t) {
+        const uint64_t dep = (m >> (t - 2)) | (m >> (t - 7)) | (m >> (t - 15)) | (m >> (t - 16));
+        if (dep & 1) m |= 1ull << t;
+    }
+    return m;
+}
+constexpr int first_vary(uint32_t vm) {
+    int i = 0;
+    while (i < 16 && !((vm >> i) & 1)) ++i;
+    return i;
+}
+
+struct State { uint32_t a, b, c, d, e, f, g, h; };
+
+// One round I of a message block.  VM marks the message words that vary
+// from one evaluation to the next: across lanes for a one-shot compression,
+// across iterations of the enclosing nonce loop for the tiled kernel (words
+// that vary across lanes but not across the loop are loop-invariant and, as
+// plain C, hoisted out of it).  SW >= 0 names a word whose sigma0 the caller
+// supplies as s0w: sigma0 is XOR-linear, so for a word built from bit-disjoint
+// lane and loop parts, sigma0(lane | loop) = sigma0(lane) ^ sigma0(loop) costs
+// one XOR per iteration instead of four instructions.
+template <uint32_t VM, int SW, int I>
+DEV void round_step(State& s, uint32_t m[16], uint32_t s0w) {
+    constexpr uint64_t WV = sched_vary(VM);
+    constexpr int F = first_vary(VM);
+    uint32_t w;
+    if constexpr (I < 16) {
+        w = m[I];
+    } else {
+        constexpr bool v2 = (WV >> (I - 2)) & 1, v7 = (WV >> (I - 7)) & 1;
+        constexpr bool v15 = (WV >> (I - 15)) & 1, v16 = (WV >> (I - 16)) & 1;
+        // uniform terms summed first (scalar), lane-varying terms after
+        uint32_t u = 0, v = 0;
+        const uint32_t t2 = ssig1<v2>(m[(I - 2) & 15]);
+        uint32_t t15;
+        if constexpr (I - 15 == SW) t15 = s0w;
+        else t15 = ssig0<v15>(m[(I - 15) & 15]);
+        if constexpr (v2) v += t2; else u += t2;
+        if constexpr (v7) v += m[(I - 7) & 15]; else u += m[(I - 7) & 15];
+        if constexpr (v15) v += t15; else u += t15;
+        if constexpr (v16) v += m[I & 15]; else u += m[I & 15];
+        w = v + u;
+        m[I & 15] = w;
+    }
+    // a and e vary from the round after the first varying word enters
+    constexpr bool ev = I > F;
+    const uint32_t t1 = s.h + bsig1<ev>(s.e) + ch(s.e, s.f, s.g) + (kK[I] + w);
+    const uint32_t t2 = bsig0<ev>(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+template <uint32_t VM, int SW, int... I>
+DEV void rounds_seq(State& s, uint32_t m[16], uint32_t s0w, std::integer_sequence<int, I...>) {
+    (round_step<VM, SW, I>(s, m, s0w), ...);
+}
+
+// 64 rounds from state s over message m (m is clobbered into the schedule
+// window).  VM marks the varying words (see round_step), SW/s0w an optional
+// caller-supplied sigma0(m[SW]).  On return s.a = a64, s.b = a63 (= b64),
+// the rest as well.
+template <uint32_t VM, int SW = -1>
+DEV void sha_rounds(State& s, uint32_t m[16], uint32_t s0w = 0) {
+    rounds_seq<VM, SW>(s, m, s0w, std::make_integer_sequence<int, 64>{});
+}
+
+template <int I>
+DEV void round_kw(State& s, uint32_t kw) {
+    // INV_STATE: round 0 of a block whose start state is invariant in the
+    // caller's loop -- plain C lets the compiler hoist its Sigma functions
+    constexpr bool v = I > 0;
+    const uint32_t t1 = s.h + bsig1<v>(s.e) + ch(s.e, s.f, s.g) + kw;
+    const uint32_t t2 = bsig0<v>(s.a) + maj(s.a, s.b, s.c);
+    s.h = s.g; s.g = s.f; s.f = s.e; s.e = s.d + t1;
+    s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
+}
+
+template <bool INV_STATE, int... I>
+DEV void rounds_kw_seq(State& s, const uint32_t* __restrict__ kw,
+                       std::integer_sequence<int, I...>) {
+    (round_kw<INV_STATE ? I : I + 1>(s, kw[I]), ...);
+}
+
+// 64 rounds over a constant block given as K[i]+W[i] (wave-uniform).
+// INV_STATE: the start state s does not change across the caller's loop.
+template <bool INV_STATE = false>
+DEV void sha_rounds_kw(State& s, const uint32_t* __restrict__ kw) {
+    rounds_kw_seq<INV_STATE>(s, kw, std::make_integer_sequence<int, 64>{});
+}
+
+// Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
+DEV void wave_min(uint64_t& k, uint64_t& n) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, off, kWaveSize);
+        const uint64_t n2 = __shfl_xor(n, off, kWaveSize);
+        const bool take = (k2 < k) || (k2 == k && n2 < n);
+        k = take ? k2 : k;
+        n = take ? n2 : n;
+    }
+}
+
+// Wrapping sum across the 64 lanes; every lane gets it.
+DEV uint64_t wave_sum(uint64_t x) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, kWaveSize);
+    return x;
+}
+
+// Checked scans: lane 0 stores the wave's (sum of keys, count) coverage pair.
+DEV void store_sums(uint64_t* sums, uint32_t wslot, uint64_t sum, uint64_t cnt) {
+    sum = wave_sum(sum);
+    cnt = wave_sum(cnt);
+    if (__lane_id() == 0) {
+        sums[2 * wslot] = sum;
+        sums[2 * wslot + 1] = cnt;
+    }
+}
+
+DEV void put_byte(uint32_t* w, uint32_t pos, uint32_t byte) {
+    w[pos >> 2] |= byte << (24u - 8u * (pos & 3u));
+}
+
+}  // namespace hm

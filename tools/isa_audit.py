@@ -4,7 +4,8 @@ mix of the innermost loop body (one iteration = 64 nonces per wave for the
 tiled and chained kernels).
 
 usage: make -C distributed_bitcoinminer_amd/csrc asm
-       python tools/isa_audit.py build/hipminer/kernels.s > profiles/r01/isa_audit.txt
+       python tools/isa_audit.py build/hipminer/scan_kernels.aligned.s > profiles/r01/isa_audit.txt
+(the scan kernels as shipped, after the placement pass align_loops.py)
 
 model_cyc prices the loop with the measured gfx950 issue costs of DESIGN.md
 §4 (half-rate 4.28, full-rate 3.45 cycles per wave64 instruction in a mixed
@@ -57,8 +58,8 @@ def main(path):
         m = re.match(r"^(_ZN2hm\w+):", l)
         if m:
             starts[m.group(1)] = i
-    print("gfx950 ISA audit of distributed_bitcoinminer_amd/csrc/kernels.hip "
-          "(hipcc -O3, ROCm 7.2; tools/isa_audit.py)")
+    print("gfx950 ISA audit of distributed_bitcoinminer_amd/csrc/scan_kernels.hip "
+          "(hipcc -O3, ROCm 7.2, after align_loops.py; tools/isa_audit.py)")
     print("inner loop = the per-nonce-iteration body (64 nonces per wave per iteration)\n")
     for sym in sorted(starts):
         if sym not in meta:
