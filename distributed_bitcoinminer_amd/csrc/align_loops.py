@@ -10,17 +10,23 @@ edit of the kernels could move a kernel by +-5 %.  MI355X_MICROARCH.md
 ("Code-placement sensitivity of hand-written streams") reports the same
 effect for hand-written asm.
 
+A second measured effect: beside half-rate ops, 4-byte (VOP2) full-rate ops
+cost more than their 8-byte (VOP3, e64) encodings at 4 mod 8 -- a
+half-rate + two full-rate pattern ran at 3.98 cycles per instruction with
+v_add_u32_e32 and 3.32 with v_add_u32_e64 (tools/place_ubench.hip).
+
 This pass makes the placement deliberate.  For every kernel whose innermost
-loop holds >= MIN_LOOP instructions it walks the loop in address order and,
-whenever an 8-byte VALU instruction would start at 0 mod 8, shifts it by 4:
-by re-encoding the nearest preceding 4-byte VALU instruction of a full-rate
-kind (v_add_u32, v_xor_b32, ... e32 -> e64: the same operation and issue
-cost in 8 bytes), or, when there is none since the previous 8-byte VALU
-instruction, by inserting `s_nop 0` in front of it.  Nothing else changes:
+loop holds >= MIN_LOOP instructions it first re-encodes every full-rate
+4-byte VALU op of the loop that has an e64 form of the same rate (v_add_u32,
+v_xor_b32, v_lshrrev_b32, ...: same operation, 8 bytes).  It then walks the
+loop in address order and, whenever an 8-byte VALU instruction would start
+at 0 mod 8 (behind an odd run of the remaining 4-byte instructions, which
+are scalar ops), moves a 4-byte VALU op behind it when the two are
+independent, or inserts `s_nop 0` in front of it.  Nothing else changes:
 the same instructions, registers, order and waits.
 
-usage: align_loops.py <in.s> <out.s> [--report] [--phase 4|0] [--no-nop]
-(--phase 0 and --no-nop are for placement experiments only.)
+usage: align_loops.py <in.s> <out.s> [--report] [--phase 4|0] [--no-nop] [--keep-e32]
+(--phase 0, --no-nop and --keep-e32 are for placement experiments only.)
 The input is `hipcc --cuda-device-only -S` output for gfx950; the output is
 assembled into the code object that api.cpp loads (see the Makefile).  The
 pass re-assembles its output and fails unless every 8-byte VALU instruction
@@ -37,7 +43,8 @@ MIN_LOOP = 500
 LATCH_BYTES = 64  # a latch block placed in front of the loop header
 PROMOTE = {"v_add_u32_e32": "v_add_u32_e64", "v_xor_b32_e32": "v_xor_b32_e64",
            "v_or_b32_e32": "v_or_b32_e64", "v_and_b32_e32": "v_and_b32_e64",
-           "v_sub_u32_e32": "v_sub_u32_e64", "v_mov_b32_e32": "v_mov_b32_e64"}
+           "v_sub_u32_e32": "v_sub_u32_e64", "v_mov_b32_e32": "v_mov_b32_e64",
+           "v_lshrrev_b32_e32": "v_lshrrev_b32_e64"}
 INST = re.compile(r"^\s+([a-z][a-z0-9_]*)(\s|$)")
 FUNC = re.compile(r"^(_Z\w+):")
 DIS = re.compile(r"^\s+(\S+)\s*(.*?)\s*//\s*([0-9A-F]+):((?:\s[0-9A-F]{8})+)"
@@ -127,6 +134,7 @@ def hot_loop(insts, heads):
 
 PHASE = 4  # target start address mod 8 of 8-byte VALU instructions
 NO_NOP = False
+ALL_E64 = True  # re-encode every full-rate 4-byte VALU op of the loop
 
 
 def stats(insts, lo, hi):
@@ -176,6 +184,18 @@ def plan_fixes(insts, lo, hi, text):
     8-byte instruction when the two are independent; else insert s_nop."""
     order = list(range(lo, hi + 1))
     promote, nops = set(), set()
+    if ALL_E64:
+        # every full-rate 4-byte VALU op becomes its 8-byte e64 form first
+        promote = {k for k in order if insts[k][1] == 4 and insts[k][2] in PROMOTE}
+        insts = list(insts)
+        shift = 0
+        for k in range(lo, len(insts)):
+            a, size, op, tgt = insts[k]
+            if k in promote:
+                insts[k] = (a + shift, 8, PROMOTE[op], tgt)
+                shift += 4
+            else:
+                insts[k] = (a + shift, size, op, tgt)
     addr = insts[lo][0]
     pos = 0
     gap = []  # positions (in order) of 4-byte instructions since the last 8-byte VALU
@@ -217,12 +237,13 @@ def plan_fixes(insts, lo, hi, text):
 
 
 def main():
-    global PHASE, NO_NOP
+    global PHASE, NO_NOP, ALL_E64
     src, dst = sys.argv[1], sys.argv[2]
     report = "--report" in sys.argv
     if "--phase" in sys.argv:
         PHASE = int(sys.argv[sys.argv.index("--phase") + 1])
     NO_NOP = "--no-nop" in sys.argv
+    ALL_E64 = "--keep-e32" not in sys.argv
     with open(src) as f:
         lines = f.read().split("\n")
     with tempfile.TemporaryDirectory() as td:

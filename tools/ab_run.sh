@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/ab; mkdir -p $O
 M=$(python -c "import random;r=random.Random(440);print(''.join(chr(r.choice(range(0x21,0x7f))) for _ in range(120)))")
-timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_none.so build/ab/lib_align.so build/ab/lib_nonop.so build/ab/lib_flip.so > $O/cfg2.txt 2>&1 &&
-timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_none.so build/ab/lib_align.so build/ab/lib_nonop.so build/ab/lib_flip.so -- bradfitz 100000000000 117179869183 > $O/d12.txt 2>&1 &&
-timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_none.so build/ab/lib_align.so build/ab/lib_nonop.so build/ab/lib_flip.so -- "$M" 0 4294967295 > $O/cfg3.txt 2>&1
+timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_align.so build/ab/lib_align2.so build/ab/lib_e64.so > $O/cfg2.txt 2>&1 &&
+timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_align.so build/ab/lib_align2.so build/ab/lib_e64.so -- bradfitz 100000000000 117179869183 > $O/d12.txt 2>&1 &&
+timeout -k 10 200 python tools/ab_libs.py 6 build/ab/lib_align.so build/ab/lib_align2.so build/ab/lib_e64.so -- "$M" 0 4294967295 > $O/cfg3.txt 2>&1
 rc=$?; tail -n 2 $O/*.txt; exit $rc
