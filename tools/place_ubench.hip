@@ -23,6 +23,8 @@ constexpr int ITERS = 1024;
 #define R(i) B(i) A(i)
 #define U(i) A(i) D(i) D(i)
 #define V(i) A(i) E(i) E(i)
+#define Y(i) A(i) B(i) B(i)
+#define Z(i) A(i) A(i) B(i)
 #define P0 ".p2align 3\n\t"
 #define P4 ".p2align 3\n\t" N
 #define OUTS "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3), "+v"(x4), "+v"(x5), "+v"(x6), "+v"(x7)
@@ -67,6 +69,13 @@ __device__ __forceinline__ int pat(uint32_t& x0, uint32_t& x1, uint32_t& x2, uin
     // same with the full-rate ops as 8-byte e64 (A E E)
     if constexpr (P == 23) { asm volatile(P0 X8(V) : OUTS : INS); return 24; }
     if constexpr (P == 24) { asm volatile(P4 X8(V) : OUTS : INS); return 24; }
+    // grouping of half-rate (A, T) and full-rate (B, E) 8-byte ops, all @4
+    if constexpr (P == 25) { asm volatile(P4 A(0) A(1) B(2) B(3) A(4) A(5) B(6) B(7) A(0) A(1) B(2) B(3) A(4) A(5) B(6) B(7) : OUTS : INS); return 16; }
+    if constexpr (P == 26) { asm volatile(P4 A(0) A(1) A(2) A(3) B(4) B(5) B(6) B(7) A(0) A(1) A(2) A(3) B(4) B(5) B(6) B(7) : OUTS : INS); return 16; }
+    if constexpr (P == 27) { asm volatile(P4 X8(Y) : OUTS : INS); return 24; }
+    if constexpr (P == 28) { asm volatile(P4 X8(Z) : OUTS : INS); return 24; }
+    if constexpr (P == 29) { asm volatile(P4 T(0) E(1) T(2) E(3) T(4) E(5) T(6) E(7) T(0) E(1) T(2) E(3) T(4) E(5) T(6) E(7) : OUTS : INS); return 16; }
+    if constexpr (P == 30) { asm volatile(P4 X8(A) X8(B) : OUTS : INS); return 16; }
     return 0;
 }
 template <int P>
@@ -84,7 +93,10 @@ __global__ void __launch_bounds__(256) kern(uint32_t* out, uint64_t* clk, uint32
     if (threadIdx.x == 0) { clk[2 * blockIdx.x] = t1 - t0; clk[2 * blockIdx.x + 1] = r1 - r0; }
 }
 template <int P>
-constexpr int pat_count() { return (P == 16 || P == 17 || P == 18 || P == 19 || P == 20) ? 32 : (P >= 21 && P <= 24) ? 24 : 16; }
+constexpr int pat_count() {
+    return (P == 16 || P == 17 || P == 18 || P == 19 || P == 20) ? 32
+         : ((P >= 21 && P <= 24) || P == 27 || P == 28) ? 24 : 16;
+}
 template <int P>
 int run(const char* name, int wpsimd, int cus, uint32_t* out, uint64_t* clk) {
     int grid = wpsimd * cus;
@@ -106,7 +118,7 @@ int main() {
     hipDeviceProp_t p; CHK(hipGetDeviceProperties(&p, 0));
     int cus = p.multiProcessorCount;
     uint32_t* out; uint64_t* clk; CHK(hipMalloc(&out, 8192 * 256 * 4)); CHK(hipMalloc(&clk, 8192 * 16));
-    for (int w : {2, 5}) {
+    for (int w : {5}) {
         run<0>("alignbit (8B) @0", w, cus, out, clk);
         run<1>("alignbit (8B) @4", w, cus, out, clk);
         run<2>("bitop3 (8B) @0", w, cus, out, clk);
@@ -132,6 +144,12 @@ int main() {
         run<22>("A D4 D4, A @4", w, cus, out, clk);
         run<23>("A E8 E8 @0", w, cus, out, clk);
         run<24>("A E8 E8 @4", w, cus, out, clk);
+        run<25>("AABB @4", w, cus, out, clk);
+        run<26>("AAAABBBB @4", w, cus, out, clk);
+        run<27>("ABB @4", w, cus, out, clk);
+        run<28>("AAB @4", w, cus, out, clk);
+        run<29>("add3/add_e64 alt @4", w, cus, out, clk);
+        run<30>("8A then 8B @4", w, cus, out, clk);
     }
     return 0;
 }
