@@ -72,6 +72,8 @@ struct Device {
     uint64_t* gathered = nullptr;  // [ndev][kMaxBatch][2] (RCCL merge)
     hm_result* host_out = nullptr; // pinned [kMaxBatch]
     hipEvent_t join[kStreams] = {};
+    hipEvent_t gate = nullptr;     // stream 0 reached its last dominant segment
+    hipEvent_t t0 = nullptr;       // timing origin of the current call
     std::vector<hipEvent_t> evpool;
     size_t evnext = 0;
     std::vector<Launch> launches;
@@ -105,7 +107,7 @@ struct hm_ctx {
     bool force_generic = false;
     bool merge_rccl = false;
     int grid_per_cu = 0;
-    int streams = 1;
+    int streams = kStreams;  // HM_OPT_STREAMS (tail filling by default)
     bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
     bool have_stats = false;
     hm_stats last{};
@@ -129,9 +131,15 @@ int device_init(Device& dv, int ordinal) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, ordinal));
     dv.cus = prop.multiProcessorCount;
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIPCHK(hipModuleLoadData(&dv.mod, hm_scan_code_object));
     for (int s = 0; s < kStreams; ++s) {
-        HIPCHK(hipStreamCreateWithFlags(&dv.stream[s], hipStreamNonBlocking));
+        // stream 0 (the dominant kernel's segments) at the highest priority,
+        // the others at the lowest: their workgroups only fill what the
+        // dominant persistent launch leaves free, i.e. its tail
+        HIPCHK(hipStreamCreateWithPriority(&dv.stream[s], hipStreamNonBlocking,
+                                           s == 0 ? prio_hi : prio_lo));
         HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
@@ -139,6 +147,8 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.sums[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
     }
+    HIPCHK(hipEventCreateWithFlags(&dv.gate, hipEventDisableTiming));
+    HIPCHK(hipEventCreate(&dv.t0));
     HIPCHK(hipMalloc(&dv.best, (size_t)kMaxBatch * kStreams * 2 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&dv.acc, (size_t)kStreams * 2 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&dv.result, (size_t)kMaxBatch * 2 * sizeof(uint64_t)));
@@ -160,6 +170,8 @@ void device_free(Device& dv) {
         if (dv.counter[s]) (void)hipFree(dv.counter[s]);
         if (dv.sums[s]) (void)hipFree(dv.sums[s]);
         if (dv.join[s]) (void)hipEventDestroy(dv.join[s]);
+        if (s == 0 && dv.gate) (void)hipEventDestroy(dv.gate);
+        if (s == 0 && dv.t0) (void)hipEventDestroy(dv.t0);
         if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
     }
     for (hipEvent_t e : dv.evpool) (void)hipEventDestroy(e);
@@ -446,29 +458,61 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     HIPCHK(hipSetDevice(dv.ordinal));
     const int n = (int)reqs.size();
     hipStream_t s0 = dv.stream[0];
+    HIPCHK(hipEventRecord(dv.t0, s0));
     HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
     HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
     if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
     HIPCHK(hipEventRecord(dv.join[0], s0));
     for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
-    // streams == 1 (default): every segment in order on stream 0, so kernels
-    // never overlap and per-kernel timings match rocprofv3.  streams > 1: the
-    // largest segment of each request on stream 0, the rest spread over 1..
+    // streams == 1: every segment in order on stream 0, so kernels never
+    // overlap and per-kernel timings match rocprofv3 exactly.  streams > 1:
+    // the segments run by the request's dominant kernel instantiation (most
+    // nonces) go first, in order, on stream 0 (high priority); the others
+    // are queued on the low-priority streams 1.., gated on stream 0 reaching
+    // its last dominant segment: they start together with that launch, get
+    // workgroup slots only as its persistent waves retire, and so run in its
+    // tail instead of after it.
     const int nstreams = std::max(1, std::min(ctx->streams, kStreams));
     int rr = 0;
     for (int r = 0; r < n; ++r) {
         if (reqs[r].empty) continue;
         std::vector<SegPlan> segs = plan_range(*reqs[r].mp, reqs[r].lo, reqs[r].hi,
                                                ctx->force_generic);
-        size_t big = 0;
-        for (size_t i = 1; i < segs.size(); ++i)
-            if (segs[i].hi - segs[i].lo > segs[big].hi - segs[big].lo) big = i;
+        // instantiation key per segment, and the key with the most nonces
+        auto key = [](const SegPlan& g) {
+            return g.kind * 1000 + g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0);
+        };
+        std::vector<std::pair<int, long double>> load;
+        for (const auto& g : segs) {
+            const long double cnt = (long double)(g.hi - g.lo) + 1;
+            auto it = std::find_if(load.begin(), load.end(),
+                                   [&](const auto& p) { return p.first == key(g); });
+            if (it == load.end()) load.push_back({key(g), cnt});
+            else it->second += cnt;
+        }
+        int dom = load.empty() ? -1 : load[0].first;
+        long double most = -1;
+        for (const auto& p : load)
+            if (p.second > most) { most = p.second; dom = p.first; }
         uint64_t* best = dv.best + (size_t)r * kStreams * 2;
-        for (size_t i = 0; i < segs.size(); ++i) {
-            int si = 0;
-            if (nstreams > 1 && i != big) si = 1 + (rr++ % (nstreams - 1));
-            int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], si, best);
-            if (rc) return rc;
+        size_t last_dom = 0;
+        for (size_t i = 0; i < segs.size(); ++i)
+            if (key(segs[i]) == dom) last_dom = i;
+        for (int pass = 0; pass < (nstreams > 1 ? 2 : 1); ++pass) {
+            if (pass == 1)
+                for (int q = 1; q < nstreams; ++q)
+                    HIPCHK(hipStreamWaitEvent(dv.stream[q], dv.gate, 0));
+            for (size_t i = 0; i < segs.size(); ++i) {
+                int si = 0;
+                if (nstreams > 1) {
+                    const bool is_dom = key(segs[i]) == dom;
+                    if (is_dom != (pass == 0)) continue;
+                    if (!is_dom) si = 1 + (rr++ % (nstreams - 1));
+                    if (is_dom && i == last_dom) HIPCHK(hipEventRecord(dv.gate, dv.stream[0]));
+                }
+                int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], si, best);
+                if (rc) return rc;
+            }
         }
     }
     for (int s = 1; s < kStreams; ++s) {
@@ -697,10 +741,31 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
                  int kind = 0, grid = 0; uint32_t comp = 0; uint64_t big = 0; };
     std::vector<Agg> aggs;
     for (auto& dv : ctx->devs) {
+        // kernel_ms: time during which some scan kernel ran on this device
+        // (union of the launches' event intervals; launches on several
+        // streams overlap)
+        std::vector<std::pair<float, float>> iv;
+        for (auto& L : dv.launches) {
+            float a = 0.f, b = 0.f;
+            HIPCHK(hipEventElapsedTime(&a, dv.t0, L.start));
+            HIPCHK(hipEventElapsedTime(&b, dv.t0, L.stop));
+            iv.push_back({a, b});
+        }
+        std::sort(iv.begin(), iv.end());
+        float cur_a = 0.f, cur_b = -1.f;
+        for (const auto& x : iv) {
+            if (x.first > cur_b) {
+                if (cur_b > cur_a) st.kernel_ms += cur_b - cur_a;
+                cur_a = x.first;
+                cur_b = x.second;
+            } else if (x.second > cur_b) {
+                cur_b = x.second;
+            }
+        }
+        if (cur_b > cur_a) st.kernel_ms += cur_b - cur_a;
         for (auto& L : dv.launches) {
             float ms = 0.f;
             HIPCHK(hipEventElapsedTime(&ms, L.start, L.stop));
-            st.kernel_ms += ms;
             st.launches += 1;
             Agg* a = nullptr;
             for (auto& x : aggs)

@@ -61,7 +61,9 @@ typedef struct hm_ctx hm_ctx;
 /* Timing and work accounting of the most recent hm_scan on a context. */
 typedef struct hm_stats {
     double wall_ms;          /* host wall time of the hm_scan call              */
-    double kernel_ms;        /* sum of scan-kernel durations (HIP events)        */
+    double kernel_ms;        /* time during which some scan kernel ran: union of
+                                the launches' HIP-event intervals, summed over
+                                devices                                          */
     double dom_kernel_ms;    /* summed duration of the dominant scan kernel's
                                 launches (dominant = most nonces; one kernel
                                 instantiation may serve several segments)       */
@@ -97,7 +99,10 @@ typedef struct hm_stats {
 #define HM_OPT_MERGE_RCCL 2    /* 1: merge multi-device candidates with RCCL     */
 #define HM_OPT_GRID_PER_CU 3   /* workgroups per CU for scan launches (0 = auto) */
 #define HM_OPT_STREAMS 4       /* HIP streams per device for segment launches
-                                  (1..4, default 1 = serial, clean profiles)   */
+                                  (1..4, default 4): the dominant kernel's
+                                  segments on a high-priority stream, the
+                                  others on low-priority streams that fill
+                                  its last launch's tail; 1 = strictly serial */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */

@@ -2,6 +2,7 @@
 segment stream count: wall GH/s of hm_scan and the dominant kernel's GH/s.
 Dev tool (runs on the GPU box)."""
 import json
+import os
 import random
 import sys
 import time
@@ -16,8 +17,8 @@ WL = {"cfg2": (b"bradfitz", 0, 2**32 - 1), "cfg3": (m120, 0, 2**32 - 1),
 c = _lib.Context([0])
 for name, (msg, lo, hi) in WL.items():
     ref = None
-    for per_cu in [2, 3, 4, 0]:
-        for streams in [1, 4]:
+    for per_cu in [int(x) for x in os.environ.get("HM_SWEEP_PER_CU", "2,3,4,0").split(",")]:
+        for streams in [int(x) for x in os.environ.get("HM_SWEEP_STREAMS", "1,4").split(",")]:
             c.set_option(_lib.HM_OPT_GRID_PER_CU, per_cu)
             c.set_option(_lib.HM_OPT_STREAMS, streams)
             walls = []
