@@ -233,7 +233,7 @@ DEV void chained_body(const ChainedArgs& A) {
         uint32_t t_end = tc * A.tch + A.tch;
         if (t_end > (uint32_t)A.pow10f) t_end = (uint32_t)A.pow10f;
         if (t_end > t_begin + piece) t_end = t_begin + piece;
-        const uint32_t* __restrict__ kw = A.kwt + (size_t)t_begin * 64;
+        const_u32* kw = (const_u32*)(A.kwt + (size_t)t_begin * 64);
         for (uint32_t t = t_begin; t < t_end; ++t, kw += 64) {
             State u = cs;
             sha_rounds_kw<true>(u, kw);

@@ -127,18 +127,21 @@ DEV void round_kw(State& s, uint32_t kw) {
     s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
 }
 
-template <bool INV_STATE, int... I>
-DEV void rounds_kw_seq(State& s, const uint32_t* __restrict__ kw,
-                       std::integer_sequence<int, I...>) {
+template <bool INV_STATE, typename KW, int... I>
+DEV void rounds_kw_seq(State& s, KW kw, std::integer_sequence<int, I...>) {
     (round_kw<INV_STATE ? I : I + 1>(s, kw[I]), ...);
 }
 
 // 64 rounds over a constant block given as K[i]+W[i] (wave-uniform).
 // INV_STATE: the start state s does not change across the caller's loop.
-template <bool INV_STATE = false>
-DEV void sha_rounds_kw(State& s, const uint32_t* __restrict__ kw) {
+template <bool INV_STATE = false, typename KW>
+DEV void sha_rounds_kw(State& s, KW kw) {
     rounds_kw_seq<INV_STATE>(s, kw, std::make_integer_sequence<int, 64>{});
 }
+
+// A table pointer in the constant address space: with a wave-uniform index
+// the compiler reads it with scalar loads (SGPR operands, no VMEM in the loop).
+typedef const __attribute__((address_space(4))) uint32_t const_u32;
 
 // Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
 DEV void wave_min(uint64_t& k, uint64_t& n) {
