@@ -121,17 +121,19 @@ std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, boo
 }
 
 double seg_cost(const SegPlan& s) {
-    // Model cycles per 64 nonces of the kernel instantiation's inner loop
-    // (tools/isa_audit.py over the gfx950 ISA, DESIGN.md §4 issue model).
+    // Measured SIMD cycles per 64 nonces of the kernel instantiation that
+    // runs the segment: 64 * 1024 SIMDs * 2.38 GHz / kernel GH/s from the
+    // layout sweep (tools/layout_perf.py, profiles/r01/session2/layout_perf.txt).
     // tiled, one block, by W1 (straddle variants differ by < 0.3 %)
-    static const double kTiled[14] = {0,    4985, 4891, 4796, 4702, 4608, 4513,
-                                      4419, 4324, 4457, 4363, 4269, 4174, 4080};
+    static const double kTiled[14] = {0,    4481, 4404, 4311, 4232, 4149, 4074,
+                                      3987, 3913, 4007, 3927, 3837, 3751, 3673};
     switch (s.kind) {
         case HM_KIND_TILED:
-            if (s.trailer) return 7680.0;  // digit block + constant trailer block (W1 13..15)
+            if (s.trailer) return 6980.0;  // digit block + constant trailer block (W1 13..15)
             return kTiled[std::min(std::max(s.W1, 1), 13)];
         case HM_KIND_CHAINED:
-            return 3472.0;  // per-lane block 0; table-driven final block
+            // per-lane block 0 amortised over 10^f table-driven final blocks
+            return s.f == 1 ? 3777.0 : 3240.0;
         default:
             // generic: every tail block per lane, no hoisting (estimate)
             return 6000.0 * s.nb;

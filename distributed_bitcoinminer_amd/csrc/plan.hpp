@@ -47,9 +47,8 @@ MsgPlan plan_message(const uint8_t* msg, uint64_t len);
 // Segment list for inclusive [lo, hi] (lo <= hi).
 std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic);
 // Modelled GPU cost of one nonce of segment s: SIMD cycles per 64 nonces of
-// the kernel instantiation that runs it, from the issue model of DESIGN.md §4
-// (half-rate 4.28, full-rate 3.45 cycles) applied to the ISA audit
-// (profiles/r01/isa_audit.txt).  Only shard balancing uses it.
+// the kernel instantiation that runs it, as measured per layout on MI355X
+// (DESIGN.md §4 "Every layout").  Only shard balancing uses it.
 double seg_cost(const SegPlan& s);
 
 struct Shard {
