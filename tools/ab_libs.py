@@ -1,5 +1,7 @@
 """Interleaved A/B of libhipminer builds in ONE process (dev tool).
-usage: python tools/ab_libs.py rounds lib1.so lib2.so ... [-- msg lo hi]"""
+usage: python tools/ab_libs.py rounds lib1.so lib2.so[:K] ... [-- msg lo hi]
+lib.so:K sets option 5 = K: the guided-self-scheduling build of the dequeue
+experiment (profiles/r01/session2/gss/); plain paths set nothing."""
 import ctypes, sys, time, json
 sys.path.insert(0, '.')
 from distributed_bitcoinminer_amd._lib import hm_result, hm_stats
@@ -10,12 +12,16 @@ if "--" in args:
 rounds, libs = int(args[0]), args[1:]
 ctxs = []
 for p in libs:
-    L = ctypes.CDLL(p)
+    path, _, k = p.partition(":")
+    L = ctypes.CDLL(path)
     L.hm_open.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     L.hm_scan.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(hm_result)]
     L.hm_scan_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats)]
     h = ctypes.c_void_p(); dev = (ctypes.c_int * 1)(0)
     assert L.hm_open(dev, 1, ctypes.byref(h)) == 0
+    if k:
+        L.hm_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]
+        assert L.hm_set_option(h, 5, int(k)) == 0
     ctxs.append((p, L, h))
 res = {p: [] for p in libs}
 ref = None
