@@ -252,6 +252,26 @@ uint32_t guided_tasks(uint64_t nunits, int grid, uint32_t* nbig) {
     return (uint32_t)(nunits - small + kSplit * small);
 }
 
+// Units of a launch over tiles [t, t+nt) (unit = lane chunk x `per_chunk`
+// loop chunks; lane value v of a tile covers nonces base + v*step + [0, step)):
+// the lane chunks of the first tile wholly below s.lo and of the last tile
+// wholly above s.hi are skipped, so shards and segments that start or end
+// inside a tile hash no out-of-range nonces beyond their edge chunks.
+// *unit0 = the first unit kept, *nunits = the count kept.
+void launch_units(const SegPlan& s, uint64_t t, uint64_t nt, uint64_t per_chunk, uint64_t step,
+                  uint32_t* unit0, uint64_t* nunits) {
+    const uint64_t P = s.pow10V;
+    const uint64_t per_tile = (uint64_t)s.tpt * per_chunk;
+    uint64_t first = 0, last = nt * per_tile - 1;
+    const uint64_t b0 = t * P;  // <= s.hi: every tile of the launch meets [lo, hi]
+    if (s.lo > b0) first = (s.lo - b0) / step / kWaveSize * per_chunk;
+    const uint64_t bl = (t + nt - 1) * P;
+    if (s.hi - bl < P - 1)
+        last = (nt - 1) * per_tile + ((s.hi - bl) / step / kWaveSize + 1) * per_chunk - 1;
+    *unit0 = (uint32_t)first;
+    *nunits = last - first + 1;
+}
+
 // nonces of [t*P, (t+nt)*P - 1] ∩ [lo, hi] (P = nonces per tile)
 uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     const uint64_t a = std::max(s.lo, t * s.pow10V);
@@ -282,7 +302,6 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         memcpy(pa.pw, mp.pw, sizeof pa.pw);
         memcpy(pa.mid, mp.mid, sizeof pa.mid);
         HIPCHK(launch_tile_plan(pa, st));
-        HIPCHK(hipMemsetAsync(dv.counter[si], 0, sizeof(unsigned int), st));
         ChainedArgs ca;
         ca.rec = dv.rec[si];
         ca.kwt = dv.kwt[si];
@@ -294,7 +313,9 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.pow10f = pow10_u64(s.f);
         ca.seg_lo = s.lo;
         ca.seg_hi = s.hi;
-        const uint64_t nunits = nt * per_tile;
+        uint32_t unit0;
+        uint64_t nunits;
+        launch_units(s, t, nt, s.ntc, pow10_u64(s.f), &unit0, &nunits);
         ca.tpt = s.tpt;
         ca.ntc = s.ntc;
         ca.tch = s.tch;
@@ -305,6 +326,11 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         if (rc) return rc;
         const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
         ca.ntasks = guided_tasks(nunits, grid, &ca.nbig);
+        // task ids start at unit0 (the queue counter too): the kernels map a
+        // task below nbig to that unit, so the skipped units are never dequeued
+        ca.ntasks += unit0;
+        ca.nbig += unit0;
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)dv.counter[si], (int)unit0, 1, st));
         Launch L;
         rc = next_event(dv, &L.start);
         if (rc) return rc;
@@ -358,7 +384,6 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             memcpy(pa.pw, mp.pw, sizeof pa.pw);
             memcpy(pa.mid, mp.mid, sizeof pa.mid);
             HIPCHK(launch_tile_plan(pa, st));
-            HIPCHK(hipMemsetAsync(dv.counter[si], 0, sizeof(unsigned int), st));
             TiledArgs ta;
             ta.rec = dv.rec[si];
             ta.counter = dv.counter[si];
@@ -368,7 +393,9 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.pow10V = s.pow10V;
             ta.seg_lo = s.lo;
             ta.seg_hi = s.hi;
-            const uint64_t nunits = nt * s.tpt;
+            uint32_t unit0;
+            uint64_t nunits;
+            launch_units(s, t, nt, 1, 100, &unit0, &nunits);
             ta.tpt = s.tpt;
             ta.vmax = (uint32_t)(pow10_u64(s.q) - 1);
             ta.q = s.q;
@@ -380,7 +407,9 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             int rc = scan_fn(dv, tiled_symbol(s, ctx->csum), &fn);
             if (rc) return rc;
             const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
-            ta.ntasks = guided_tasks(nunits, grid, &ta.nbig);
+            ta.ntasks = guided_tasks(nunits, grid, &ta.nbig) + unit0;  // see enqueue_chained
+            ta.nbig += unit0;
+            HIPCHK(hipMemsetD32Async((hipDeviceptr_t)dv.counter[si], (int)unit0, 1, st));
             Launch L;
             rc = next_event(dv, &L.start);
             if (rc) return rc;

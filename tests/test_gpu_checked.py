@@ -113,6 +113,31 @@ def test_checked_guided_split_boundaries(ctx):
     assert whole == _generic(ctx, b"bradfitz", base, base + 80_000_000)
 
 
+def _long120():
+    rng = random.Random(440)
+    return bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
+
+
+@pytest.mark.parametrize("msg", [b"bradfitz", _long120()], ids=["tiled", "chained"])
+def test_checked_shard_edges_mid_tile(ctx, msg):
+    """A weak-scaling shard of the bench (rank 3 of 8: [3*2^32, 4*2^32), d=11)
+    starts and ends inside a tile (10^8 nonces for bradfitz).  The launch skips
+    the lane chunks of its edge tiles that lie wholly outside the range; the
+    count stays exact, cuts inside the first and last lane chunks and tiles add
+    up, and windows at both edges match the generic kernel."""
+    lo, hi = 3 << 32, (4 << 32) - 1
+    seg = _lib.debug_plan(msg, lo, hi)[0]
+    assert seg["kind"] in (_lib.HM_KIND_TILED, _lib.HM_KIND_CHAINED) and seg["d"] == 11
+    whole = ctx.scan_checked(msg, lo, hi)
+    assert whole[2] == hi - lo + 1
+    P = 10 ** seg["V"]
+    cuts = [lo, lo + 1, lo + 6399, lo + 6400 * 65 + 17, (lo // P + 1) * P, hi // P * P - 1,
+            hi - 6400 * 3, hi, hi + 1]
+    assert _add([ctx.scan_checked(msg, a, b - 1) for a, b in zip(cuts, cuts[1:])]) == whole
+    for w_lo, w_hi in ((lo, lo + 3_000_000), (hi - 3_000_000, hi)):
+        assert ctx.scan_checked(msg, w_lo, w_hi) == _generic(ctx, msg, w_lo, w_hi)
+
+
 def _large():
     with open(os.path.join(os.path.dirname(__file__), "golden", "large.json")) as f:
         return [c for c in json.load(f) if "sum" in c]
