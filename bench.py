@@ -220,6 +220,14 @@ def main():
         ops_per_launch = st["dom_nonces"] / launches * OPS_PER_COMPRESSION * C
         achieved = ops_per_launch / (avg_ms * 1e-3) / 1e12
         traffic, f_eff, traffic_src = profiled(st["dom_kernel"])
+        # algorithmic HBM bytes of one dominant launch: its 128-B tile records
+        # (10^V nonces each) + one 16-B candidate per wave of the grid; the
+        # work queue adds one device-scope atomicAdd per dequeued task
+        dom_seg = max(_lib.debug_plan(msg, lo, hi), key=lambda s: s["hi"] - s["lo"])
+        nonces_pl = st["dom_nonces"] // launches
+        tiles_pl = -(-nonces_pl // 10 ** dom_seg["V"])
+        algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
+        tasks_pl = nonces_pl // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
         line = {
             "metric": "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of INT32 VALU roofline",
             "value": round(value, 3),
@@ -244,6 +252,12 @@ def main():
                          "frac": round(achieved / PEAK_TOPS, 4), "traffic": traffic,
                          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                          "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "queue_atomics_per_launch": tasks_pl,
+                         "traffic_note": "PMC traffic is the work queue's device-scope atomics "
+                                         "(one per dequeued task, executed memory-side), not "
+                                         "re-reads; cutting them 4x cut WRITE_SIZE 4x but cost "
+                                         "kernel rate (DESIGN.md §9)",
                          "f_eff_ghz": f_eff,
                          "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
                          "kernel": st["dom_kernel"],
