@@ -1,6 +1,6 @@
 """MI355X-native miner backend for alexsun705/distributed_bitcoinMiner's min-hash scan.
 
-The hot path is the miner's scan (cmu440/bitcoin/miner/miner.go:63-76 calling
+The hot path is the miner's scan (cmu440/bitcoin/miner/miner.go:46-59 calling
 bitcoin.Hash, cmu440/bitcoin/hash.go:13-17).  It runs as hand-written gfx950
 HIP kernels behind the C ABI in include/hipminer.h (libhipminer.so); this
 package mirrors the reference's Go interface on top of that ABI:

@@ -130,7 +130,7 @@ def _fix_surrogates(s: str) -> str:
 
 def unmarshal(data: bytes) -> tuple[Message, Exception | None]:
     """json.Unmarshal into a zero Message: case-insensitive keys, unknown keys
-    ignored, the error returned (the miner ignores it, miner.go:62)."""
+    ignored, the error returned (the miner ignores it, miner.go:45)."""
     m = Message()
     try:
         # Go replaces invalid UTF-8 in JSON strings with U+FFFD

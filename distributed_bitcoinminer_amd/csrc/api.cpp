@@ -1,7 +1,7 @@
 // api.cpp -- the hipminer C ABI (include/hipminer.h).
 //
 // Replaces, inside the Go miner process, the scan of evalRoutine
-// (cmu440/bitcoin/miner/miner.go:63-76) and bitcoin.Hash
+// (cmu440/bitcoin/miner/miner.go:46-59) and bitcoin.Hash
 // (cmu440/bitcoin/hash.go:13-17).  Per device and per call:
 //
 //   host:  plan_message (midstate) -> plan_range (digit segments, layouts)

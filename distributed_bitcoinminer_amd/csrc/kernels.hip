@@ -7,7 +7,7 @@
 //                        block for each loop value.
 //   hm_fold_kernel       second reduce pass (candidates -> 16-B best).
 //   hm_sum_fold_kernel   coverage sums of checked scans (per wave -> total).
-//   hm_init_best_kernel  (MaxUint64, 0) seeds (miner.go:65-66).
+//   hm_init_best_kernel  (MaxUint64, 0) seeds (miner.go:48-49).
 //
 // The scan kernels themselves are in scan_kernels.hip (own code object).
 #include <hip/hip_runtime.h>
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(kBlock) hm_sum_fold_kernel(const uint64_t* __r
 
 __global__ void hm_init_best_kernel(uint64_t* best, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) { best[2 * i] = ~0ull; best[2 * i + 1] = 0; }  // (MaxUint64, 0): miner.go:65-66
+    if (i < n) { best[2 * i] = ~0ull; best[2 * i + 1] = 0; }  // (MaxUint64, 0): miner.go:48-49
 }
 
 // ---------------------------------------------------------------------------

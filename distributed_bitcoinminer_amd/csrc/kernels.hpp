@@ -1,6 +1,6 @@
 // kernels.hpp -- argument blocks and launchers of the gfx950 scan kernels.
 //
-// Hot path replaced: the miner scan loop (cmu440/bitcoin/miner/miner.go:63-76)
+// Hot path replaced: the miner scan loop (cmu440/bitcoin/miner/miner.go:46-59)
 // calling bitcoin.Hash (cmu440/bitcoin/hash.go:13-17) once per nonce.
 //
 // Work decomposition:

@@ -29,7 +29,7 @@ std::string marshal(const BitcoinMsg& m) { return hm::wire::marshal_bitcoin(m); 
 
 BitcoinMsg unmarshal(const std::string& payload) {
     BitcoinMsg m;
-    hm::wire::unmarshal_bitcoin(payload, &m);  // error ignored (miner.go:62)
+    hm::wire::unmarshal_bitcoin(payload, &m);  // error ignored (miner.go:45)
     return m;
 }
 
@@ -79,8 +79,8 @@ int main(int argc, char** argv) {
             BitcoinMsg res;
             res.type = 2;  // Result
             res.hash = ~0ull;
-            res.nonce = 0;  // miner.go:65-66
-            const uint64_t end = req.upper + 1;  // miner.go:69, wraps
+            res.nonce = 0;  // miner.go:48-49
+            const uint64_t end = req.upper + 1;  // miner.go:52, wraps
             if (req.lower < end) {
                 hm_result out;
                 rc = hm_scan(gpu, reinterpret_cast<const uint8_t*>(req.data.data()), req.data.size(),

@@ -1,6 +1,6 @@
 // scan_kernels.hip -- the gfx950 scan kernels of the min-hash nonce search.
 //
-// Replaces the miner's sequential loop (cmu440/bitcoin/miner/miner.go:63-76)
+// Replaces the miner's sequential loop (cmu440/bitcoin/miner/miner.go:46-59)
 // over bitcoin.Hash (cmu440/bitcoin/hash.go:13-17).  Integer-VALU bound: no
 // MFMA, no LDS on the hot path, ~zero HBM traffic.
 //

@@ -3,7 +3,7 @@
 //
 // The reference computes SHA-256 through Go's crypto/sha256 inside
 // bitcoin.Hash (cmu440/bitcoin/hash.go:14-16); the scan loop is
-// cmu440/bitcoin/miner/miner.go:63-76.
+// cmu440/bitcoin/miner/miner.go:46-59.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -1,17 +1,17 @@
-"""Miner-side mirror of ``evalRoutine`` (cmu440/bitcoin/miner/miner.go:53-85).
+"""Miner-side mirror of ``evalRoutine`` (cmu440/bitcoin/miner/miner.go:36-68).
 
 ``Miner.eval_request`` is one iteration of the reference's loop body
-(miner.go:61-79): unmarshal the Request (errors ignored, :62), scan
+(miner.go:44-62): unmarshal the Request (errors ignored, :45), scan
 ``[Lower, Upper]`` for the min hash and marshal ``NewResult(hash, nonce)``.
-The scan itself -- the reference's hot loop, miner.go:63-76 -- runs on the
-GPU through ``hm_scan``.  The reference's ``upper := Upper+1`` (:69) is a
+The scan itself -- the reference's hot loop, miner.go:46-59 -- runs on the
+GPU through ``hm_scan``.  The reference's ``upper := Upper+1`` (:52) is a
 uint64 add, so ``Upper == 2^64-1`` scans nothing and yields
 ``(MaxUint64, 0)``; that quirk (SURVEY A-inv-5) is reproduced here, in the
 caller, exactly as the Go shim in go/hipminer does it.
 
 There is no CPU fallback: if the GPU path fails, ``HipMinerError`` propagates
 and the miner process ends, as the reference miner does on an LSP error
-(miner.go:57-60, 80-83); the unchanged server then reassigns its chunk
+(miner.go:40-43, 63-66); the unchanged server then reassigns its chunk
 (server.go:326-376).
 """
 from __future__ import annotations
@@ -21,8 +21,8 @@ from .bitcoin import MAXU64, NewResult, marshal, unmarshal
 
 
 def eval_range(lower: int, upper: int):
-    """The scan range miner.go:67-70 actually visits, or None if empty."""
-    up = (upper + 1) & MAXU64  # miner.go:69, uint64 wrap
+    """The scan range miner.go:50-53 actually visits, or None if empty."""
+    up = (upper + 1) & MAXU64  # miner.go:52, uint64 wrap
     if not lower < up:
         return None
     return lower, up - 1
@@ -35,15 +35,15 @@ class Miner:
         self.ctx = ctx if ctx is not None else _lib.Context(devices)
 
     def scan(self, data, lower: int, upper: int) -> tuple[int, int]:
-        """(result, index) of miner.go:63-76 for Request{data, lower, upper}."""
+        """(result, index) of miner.go:46-59 for Request{data, lower, upper}."""
         rng = eval_range(lower, upper)
         if rng is None:
-            return MAXU64, 0  # miner.go:65-66 initial values, loop never runs
+            return MAXU64, 0  # miner.go:48-49 initial values, loop never runs
         return self.ctx.scan(data, rng[0], rng[1])
 
     def eval_request(self, payload: bytes) -> bytes:
         """One evalRoutine step: Request payload in, Result payload out."""
-        req, _err = unmarshal(payload)  # error ignored, miner.go:62
+        req, _err = unmarshal(payload)  # error ignored, miner.go:45
         h, n = self.scan(req.Data, req.Lower, req.Upper)
         return marshal(NewResult(h, n))
 

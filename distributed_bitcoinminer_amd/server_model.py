@@ -11,7 +11,7 @@ is; this model gives exact end-to-end expectations for GPU miners driven by it:
 * ``merge_in_arrival_order`` restates server.go:140-141 (seed
   (MaxUint64, MaxUint64)) and :273-276 (strict ``<`` in arrival order).
 * ``expected_client_result`` combines both with the miner semantics
-  (miner.go:63-76 incl. the Upper+1 wrap) for a given scan function.
+  (miner.go:46-59 incl. the Upper+1 wrap) for a given scan function.
 * ``ServerSim`` is the whole event loop of the server (server.go:207-400) as a
   deterministic state machine: FIFO of client requests, miner joins, results,
   and the drop / reassign paths for miners and clients.  Driving real GPU

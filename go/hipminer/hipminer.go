@@ -1,6 +1,6 @@
 // Package hipminer is the cgo binding of libhipminer.so (include/hipminer.h):
 // the MI355X backend for the min-hash scan of the reference miner
-// (cmu440/bitcoin/miner/miner.go:63-76, bitcoin.Hash at
+// (cmu440/bitcoin/miner/miner.go:46-59, bitcoin.Hash at
 // cmu440/bitcoin/hash.go:13-17).
 //
 // Built only where a Go toolchain exists (none in the build image); the C ABI
@@ -128,11 +128,11 @@ func (m *Miner) ScanMany(reqs []Request) ([][2]uint64, error) {
 	return res, nil
 }
 
-// EvalRequest is the drop-in for miner.go:63-76: it keeps the reference's
+// EvalRequest is the drop-in for miner.go:46-59: it keeps the reference's
 // `upper := Upper + 1` uint64 wrap (Upper == MaxUint64 scans nothing) and
 // its initial (MaxUint64, 0).
 func (m *Miner) EvalRequest(data string, lower, upper uint64) (hash, nonce uint64, err error) {
-	end := upper + 1 // wraps exactly like miner.go:69
+	end := upper + 1 // wraps exactly like miner.go:52
 	if !(lower < end) {
 		return maxUint64, 0, nil
 	}

@@ -8,7 +8,7 @@
  *   hm_hash  replaces  bitcoin.Hash(msg string, nonce uint64) uint64
  *                      cmu440/bitcoin/hash.go:13-17
  *   hm_scan  replaces  the scan loop of evalRoutine,
- *                      cmu440/bitcoin/miner/miner.go:63-76
+ *                      cmu440/bitcoin/miner/miner.go:46-59
  *                      (result = maxUint; index = 0; for i := lower; i < upper;
  *                       i++ { hash := bitcoin.Hash(data, i); if hash < result ...})
  *                      fed by bitcoin.Message{Data, Lower, Upper}
@@ -24,7 +24,7 @@
  *     [lo, hi], seeded with (UINT64_MAX, 0).  This equals the reference's
  *     ascending strict-< loop, ties to the lowest nonce.  lo > hi gives
  *     (UINT64_MAX, 0).  hi may be UINT64_MAX: the reference miner's
- *     `upper := Upper+1` wrap (miner.go:69) is NOT applied here; callers that
+ *     `upper := Upper+1` wrap (miner.go:52) is NOT applied here; callers that
  *     mirror evalRoutine apply it (see distributed_bitcoinminer_amd/miner.py).
  *
  * Ownership: msg is borrowed for the call only (never retained), so a cgo

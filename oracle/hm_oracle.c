@@ -18,7 +18,7 @@
  *     Go's crypto/sha256 (stdlib, unpinned version; the staff binaries were
  *     built with go1.10.3); it is restated here from FIPS 180-4.
  *
- *   oracle_scan   <- cmu440/bitcoin/miner/miner.go:63-76
+ *   oracle_scan   <- cmu440/bitcoin/miner/miner.go:46-59
  *       result = maxUint; index = 0                               (:65-66)
  *       for i := lower; i < upper; i++ { if hash < result {...} } (:70-76)
  *     over the truly inclusive range [lo, hi] (hi may be 2^64-1).  Ties keep
@@ -26,7 +26,7 @@
  *     range into contiguous chunks and merge lexicographically on
  *     (hash, nonce), which is equivalent to one ascending strict-< scan.
  *
- *   oracle_miner_eval <- miner.go:67-76 including the `upper := Upper+1`
+ *   oracle_miner_eval <- miner.go:50-59 including the `upper := Upper+1`
  *     wrap (:69): Upper == 2^64-1 scans nothing and returns (MaxUint64, 0).
  *
  * Parity status: the reference ships no golden vectors for this path and its
@@ -136,7 +136,7 @@ typedef struct {
     uint64_t sum, count; /* coverage checksum: wrapping sum of keys, nonces hashed */
 } o_job;
 
-/* miner.go:65-76 over inclusive [lo, hi], strict <, ascending. */
+/* miner.go:48-59 over inclusive [lo, hi], strict <, ascending. */
 static void *o_scan_job(void *arg) {
     o_job *j = (o_job *)arg;
     uint64_t result = MAXU64, index = 0, sum = 0, count = 0;
@@ -161,7 +161,7 @@ static void *o_scan_job(void *arg) {
 }
 
 /* Inclusive scan [lo, hi] (hi may be 2^64-1).  lo > hi is an empty range and
- * returns (MaxUint64, 0), the miner's initial value (miner.go:65-66).
+ * returns (MaxUint64, 0), the miner's initial value (miner.go:48-49).
  * Also returns the coverage checksum that hm_scan_checked computes on the
  * GPU: the wrapping (mod 2^64) sum of every key and the number of nonces. */
 void oracle_scan_sum(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int threads,
@@ -208,7 +208,7 @@ void oracle_scan(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int t
     oracle_scan_sum(msg, len, lo, hi, threads, out_hash, out_nonce, &s, &c);
 }
 
-/* miner.go:67-76 verbatim semantics, including `upper := Upper + 1` wrapping
+/* miner.go:50-59 verbatim semantics, including `upper := Upper + 1` wrapping
  * to 0 when Upper == MaxUint64 (then the loop runs zero times). */
 void oracle_miner_eval(const uint8_t *msg, size_t len, uint64_t lower, uint64_t upper_incl,
                        int threads, uint64_t *out_hash, uint64_t *out_nonce) {

@@ -8,7 +8,7 @@ Two independent restatements of the reference hot path live here
 (paths relative to /root/reference, cmu440/ = p1/src/github.com/cmu440/):
 
 * ``py_hash`` / ``py_scan``: pure Python over ``hashlib`` (OpenSSL's SHA-256),
-  restating ``cmu440/bitcoin/hash.go:13-17`` and ``miner/miner.go:63-76``.
+  restating ``cmu440/bitcoin/hash.go:13-17`` and ``miner/miner.go:46-59``.
   Slow (~1 MH/s); used for golden fixtures and small cases.
 * ``c_hash`` / ``c_scan`` / ``c_miner_eval``: ctypes over ``oracle/build/
   liboracle.so`` (``oracle/hm_oracle.c``: its own FIPS 180-4 SHA-256 and the
@@ -70,7 +70,7 @@ def py_hash(msg, nonce: int) -> int:
 
 
 def py_scan(msg, lo: int, hi: int):
-    """miner.go:65-76 over inclusive [lo, hi]: strict <, ascending, init (MAX, 0)."""
+    """miner.go:48-59 over inclusive [lo, hi]: strict <, ascending, init (MAX, 0)."""
     result, index = MAXU64, 0
     m = _b(msg)
     for i in range(lo, hi + 1):
@@ -81,7 +81,7 @@ def py_scan(msg, lo: int, hi: int):
 
 
 def py_miner_eval(msg, lower: int, upper: int):
-    """miner.go:67-76 with the `upper := Upper+1` uint64 wrap (:69)."""
+    """miner.go:50-59 with the `upper := Upper+1` uint64 wrap (:52)."""
     up = (upper + 1) & MAXU64
     if not lower < up:
         return MAXU64, 0

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Generate the golden fixtures in tests/golden/ (run in the build container).
 
-The reference (Go; cmu440/bitcoin/hash.go:13-17 + miner/miner.go:63-76) cannot
+The reference (Go; cmu440/bitcoin/hash.go:13-17 + miner/miner.go:46-59) cannot
 run here -- no Go toolchain -- and its own tests hold no vectors for the hash
 or the scan.  These fixtures therefore come from this
 self-contained restatement over Python's ``hashlib`` (OpenSSL SHA-256, an
@@ -9,7 +9,7 @@ implementation independent of both oracle/hm_oracle.c and the HIP kernels):
 
   Hash(msg, n)  = BigEndian.Uint64(SHA256(msg ‖ " " ‖ decimal(n))[:8])
   scan(lo, hi)  = ascending strict-< min over inclusive [lo, hi], init (MAX, 0)
-  miner_eval    = scan with miner.go:69's `upper := Upper+1` uint64 wrap
+  miner_eval    = scan with miner.go:52's `upper := Upper+1` uint64 wrap
 
 The FIPS 180-4 / NIST known answers in fips_kats are published constants and
 pin the SHA-256 underneath.

@@ -1,5 +1,5 @@
 """Host mirror of the reference interface: Message JSON wire form (message.go +
-encoding/json), the miner's Request -> Result step (miner.go:61-79) with its
+encoding/json), the miner's Request -> Result step (miner.go:44-62) with its
 Upper+1 wrap, and the planner's segment layouts."""
 import pytest
 

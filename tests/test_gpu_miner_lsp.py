@@ -45,7 +45,7 @@ def test_miner_join_and_requests(oracle_mod, golden):
         assert _ask(srv, cid, m, 19970000, 19971000) == oracle_mod.c_scan(m, 19970000, 19971000)
         weird = 'a<b>&"é '.encode()
         assert _ask(srv, cid, weird, 5, 5000) == oracle_mod.c_scan(weird, 5, 5000)
-        # malformed Requests: decode errors are ignored (miner.go:62), so the
+        # malformed Requests: decode errors are ignored (miner.go:45), so the
         # miner scans the zero Request [0, 0] of "" or the fields that decoded
         for payload, exp in [(b"garbage", (oracle_mod.c_hash(b"", 0), 0)),
                              (b'{"Data":"abc","Lower":5,"Upper":"x"}', (MAX, 0)),

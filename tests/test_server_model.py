@@ -48,7 +48,7 @@ def _results(writes):
 
 
 class _Fleet:
-    """Miners that answer with the CPU oracle's miner_eval (miner.go:63-76)."""
+    """Miners that answer with the CPU oracle's miner_eval (miner.go:46-59)."""
 
     def __init__(self, oracle_mod):
         self.o = oracle_mod

@@ -2,7 +2,7 @@
 behind LSP, as the reference client -> server -> miner chain drives it.
 
 The client's `bradfitz 10000000` reaches the miner as Request [0, 10^7+1]
-(server.go:169 adds one; miner.go:69 scans inclusively).  A fake LSP server
+(server.go:169 adds one; miner.go:52 scans inclusively).  A fake LSP server
 (tests/lsp_harness.py, the role of the reference server / staff mtest) sends
 that Request to a native `hm_miner` process (csrc/miner_main.cpp) and times
 Request-write -> Result-read, i.e. JSON + LSP framing both ways over
