@@ -62,7 +62,9 @@ WORKLOADS = {
 def profiled(kernel: str):
     """PMC summary of `kernel` from the newest committed profile
     (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py):
-    HBM bytes per launch and the effective clock, with the file it came from."""
+    HBM bytes per launch, the effective clock and the measured VALU
+    instructions per nonce (SQ_INSTS_VALU per 64-nonce wave iteration), with
+    the file they came from."""
     import glob
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
                        reverse=True):
@@ -71,8 +73,8 @@ def profiled(kernel: str):
         if kernel in summ:
             k = summ[kernel]
             return k["hbm_bytes_per_launch"], k["f_eff_ghz_largest_dispatch"], \
-                os.path.relpath(path, ROOT)
-    return None, None, None
+                k.get("valu_insts_per_wave_iteration_64_nonces"), os.path.relpath(path, ROOT)
+    return None, None, None, None
 
 
 OPS_PER_COMPRESSION = 1552
@@ -219,7 +221,7 @@ def main():
         avg_ms = st["dom_kernel_ms"] / launches
         ops_per_launch = st["dom_nonces"] / launches * OPS_PER_COMPRESSION * C
         achieved = ops_per_launch / (avg_ms * 1e-3) / 1e12
-        traffic, f_eff, traffic_src = profiled(st["dom_kernel"])
+        traffic, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
         # algorithmic HBM bytes of one dominant launch: its 128-B tile records
         # (10^V nonces each) + one 16-B candidate per wave of the grid; the
         # work queue adds one device-scope atomicAdd per dequeued task
@@ -265,6 +267,7 @@ def main():
                          "avg_launch_ms": round(avg_ms, 3),
                          "nonces_per_launch": st["dom_nonces"] // launches,
                          "ops_per_nonce": OPS_PER_COMPRESSION * C,
+                         "valu_instr_per_nonce_pmc": round(valu_pmc, 1) if valu_pmc else None,
                          "kernel_GHs": round(st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
