@@ -43,6 +43,20 @@ namespace {
 
 constexpr int kStreams = 4;
 
+// No C++ exception crosses the C ABI (include/hipminer.h): the entry points
+// run their bodies through guarded(), which maps an escaping exception
+// (std::bad_alloc from the planner's vectors, anything else) to a return code.
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return HM_ERR_NOMEM;
+    } catch (...) {
+        return HM_ERR_INTERNAL;
+    }
+}
+
 struct Launch {
     hipEvent_t start, stop;
     uint64_t nonces;
@@ -646,6 +660,8 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
     return HM_OK;
 }
 
+int open_devices(const int* devices, int ndev, hm_ctx** out);
+
 }  // namespace
 
 extern "C" {
@@ -661,14 +677,16 @@ int hm_version(void) { return (1 << 16) | 3; }
 int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t* bounds) {
     if (n <= 0 || !bounds || (len > 0 && !msg)) return HM_ERR_INVALID;
-    static const uint8_t empty = 0;
-    const MsgPlan mp = plan_message(msg ? msg : &empty, msg ? len : 0);
-    const std::vector<Shard> sh = partition_range(mp, lo, hi, n, false);
-    for (int i = 0; i < n; ++i) {
-        bounds[2 * i] = sh[i].empty ? 1 : sh[i].lo;
-        bounds[2 * i + 1] = sh[i].empty ? 0 : sh[i].hi;
-    }
-    return HM_OK;
+    return guarded([&] {
+        static const uint8_t empty = 0;
+        const MsgPlan mp = plan_message(msg ? msg : &empty, msg ? len : 0);
+        const std::vector<Shard> sh = partition_range(mp, lo, hi, n, false);
+        for (int i = 0; i < n; ++i) {
+            bounds[2 * i] = sh[i].empty ? 1 : sh[i].lo;
+            bounds[2 * i + 1] = sh[i].empty ? 0 : sh[i].hi;
+        }
+        return (int)HM_OK;
+    });
 }
 
 const char* hm_strerror(int rc) {
@@ -687,6 +705,14 @@ const char* hm_strerror(int rc) {
 int hm_open(const int* devices, int ndev, hm_ctx** out) {
     if (!out || ndev < 0 || (ndev > 0 && !devices)) return HM_ERR_INVALID;
     *out = nullptr;
+    return guarded([&] { return open_devices(devices, ndev, out); });
+}
+
+}  // extern "C"
+
+namespace {
+
+int open_devices(const int* devices, int ndev, hm_ctx** out) {
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return HM_ERR_NO_DEVICE;
     std::vector<int> ords;
@@ -700,18 +726,25 @@ int hm_open(const int* devices, int ndev, hm_ctx** out) {
     }
     hm_ctx* ctx = new (std::nothrow) hm_ctx;
     if (!ctx) return HM_ERR_NOMEM;
-    ctx->devs.resize(ords.size());
-    for (size_t i = 0; i < ords.size(); ++i) {
-        int rc = device_init(ctx->devs[i], ords[i]);
-        if (rc) {
-            for (auto& dv : ctx->devs) device_free(dv);
-            delete ctx;
-            return rc;
-        }
+    int rc = HM_OK;
+    try {
+        ctx->devs.resize(ords.size());
+        for (size_t i = 0; i < ords.size() && rc == HM_OK; ++i) rc = device_init(ctx->devs[i], ords[i]);
+    } catch (const std::bad_alloc&) {
+        rc = HM_ERR_NOMEM;
+    }
+    if (rc) {
+        for (auto& dv : ctx->devs) device_free(dv);
+        delete ctx;
+        return rc;
     }
     *out = ctx;
     return HM_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 void hm_close(hm_ctx* ctx) {
     if (!ctx) return;
@@ -836,7 +869,7 @@ int hm_scan_many(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
     for (int r = 0; r < n; ++r)
         if (!reqs[r].msg && reqs[r].len) return HM_ERR_INVALID;
     std::lock_guard<std::mutex> g(ctx->mu);
-    return scan_many_locked(ctx, reqs, n, outs);
+    return guarded([&] { return scan_many_locked(ctx, reqs, n, outs); });
 }
 
 int hm_scan(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
@@ -853,7 +886,7 @@ int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, ui
     hm_request q{msg, len, lo, hi};
     hm_result res;
     ctx->csum = true;
-    int rc = scan_many_locked(ctx, &q, 1, &res);
+    int rc = guarded([&] { return scan_many_locked(ctx, &q, 1, &res); });
     ctx->csum = false;
     if (rc) return rc;
     uint64_t s = 0, c = 0;
@@ -884,7 +917,12 @@ int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int 
     if (lo > hi) return 0;
     static const uint8_t empty = 0;
     const MsgPlan mp = plan_message(msg ? msg : &empty, msg ? len : 0);
-    std::vector<SegPlan> segs = plan_range(mp, lo, hi, force_generic != 0);
+    std::vector<SegPlan> segs;
+    try {
+        segs = plan_range(mp, lo, hi, force_generic != 0);
+    } catch (...) {
+        return HM_ERR_NOMEM;
+    }
     int i = 0;
     for (; i < (int)segs.size() && i < cap; ++i) {
         const SegPlan& s = segs[i];
