@@ -268,6 +268,14 @@ def main():
                          "nonces_per_launch": st["dom_nonces"] // launches,
                          "ops_per_nonce": OPS_PER_COMPRESSION * C,
                          "valu_instr_per_nonce_pmc": round(valu_pmc, 1) if valu_pmc else None,
+                         # executed lane-ops (PMC VALU instructions x 64 lanes per
+                         # 64 nonces) / peak: the issue-level fraction. The
+                         # nominal `frac` prices 1552*C ops per nonce and exceeds
+                         # 1 for the chained kernel, whose wave-uniform final
+                         # block needs no per-lane message schedule
+                         "executed_frac": round(valu_pmc * st["dom_nonces"]
+                                                / (st["dom_kernel_ms"] * 1e-3) / 1e12
+                                                / PEAK_TOPS, 4) if valu_pmc else None,
                          "kernel_GHs": round(st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9, 3)},
         }
         if world == 1 and not args.no_cpu_baseline:
