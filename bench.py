@@ -59,19 +59,34 @@ WORKLOADS = {
 }
 
 
+def code_object_sha16():
+    """sha256 (16 hex) of the scan kernels' code object this tree built
+    (build/hipminer/hipminer_scan.hsaco, embedded in libhipminer.so)."""
+    import hashlib
+    path = os.path.join(ROOT, "build", "hipminer", "hipminer_scan.hsaco")
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def profiled(kernel: str):
     """PMC summary of `kernel` from the newest committed profile
     (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py):
     HBM bytes per launch, the effective clock and the measured VALU
     instructions per nonce (SQ_INSTS_VALU per 64-nonce wave iteration), with
-    the file they came from."""
+    the file they came from.  Only a summary recorded for THIS build's code
+    object (its `code_object_sha16`) counts: a stale one gives Nones."""
     import glob
+    sha = code_object_sha16()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_summary.json")),
                        reverse=True):
         with open(path) as f:
             summ = json.load(f)
         if kernel in summ:
             k = summ[kernel]
+            if sha is None or k.get("code_object_sha16") != sha:
+                return None, None, None, None
             return k["hbm_bytes_per_launch"], k["f_eff_ghz_largest_dispatch"], \
                 k.get("valu_insts_per_wave_iteration_64_nonces"), os.path.relpath(path, ROOT)
     return None, None, None, None
@@ -123,12 +138,69 @@ def cpu_baseline(msg: bytes, name: str):
                              "sample": f"[0, {n1}) on 1 thread, {d1:.2f} s"}}
 
 
+def roofline(st, msg, lo, hi):
+    """Roofline object of the dominant scan kernel of the last hm_scan (st =
+    hm_stats).  achieved = algorithmic ops per launch / average launch time
+    (HIP events on the launch stream).  `frac` prices the compressions per
+    nonce the kernel executes (dom_compressions_eff: the chained kernel of a
+    two-block tail hoists block 0 out of its loop, SURVEY §8(d) "fraction at
+    C = 1"); `frac_algorithmic_C` prices SURVEY's 1552*C with C counted
+    before any hoisting (equal for one-block tails)."""
+    from distributed_bitcoinminer_amd import _lib
+    C = st["dom_compressions"]
+    C_eff = st["dom_compressions_eff"] or C
+    launches = max(1, st["dom_launches"])
+    avg_ms = st["dom_kernel_ms"] / launches
+    nonces_pl = st["dom_nonces"] / launches
+    achieved = nonces_pl * OPS_PER_COMPRESSION * C_eff / (avg_ms * 1e-3) / 1e12
+    achieved_alg = nonces_pl * OPS_PER_COMPRESSION * C / (avg_ms * 1e-3) / 1e12
+    traffic, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
+    # algorithmic HBM bytes of one dominant launch: its 128-B tile records
+    # (10^V nonces each) + one 16-B candidate per wave of the grid; the
+    # work queue adds one device-scope atomicAdd per dequeued task
+    dom_seg = max(_lib.debug_plan(msg, lo, hi), key=lambda s: s["hi"] - s["lo"])
+    tiles_pl = -(-int(nonces_pl) // 10 ** dom_seg["V"])
+    algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
+    tasks_pl = int(nonces_pl) // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
+    return {"bound": "valu", "achieved": round(achieved, 3),
+            "peak": round(PEAK_TOPS, 3), "unit": "T int32 lane-ops/s",
+            "frac": round(achieved / PEAK_TOPS, 4),
+            "compressions_per_nonce": round(C_eff, 6),
+            "frac_algorithmic_C": round(achieved_alg / PEAK_TOPS, 4),
+            "compressions_per_nonce_algorithmic": C,
+            "traffic": traffic,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": algo_bytes,
+            "queue_atomics_per_launch": tasks_pl,
+            "traffic_note": "PMC traffic is the work queue's device-scope atomics "
+                            "(one per dequeued task, executed memory-side), not "
+                            "re-reads; cutting them 4x cut WRITE_SIZE 4x but cost "
+                            "kernel rate (DESIGN.md §9)",
+            "f_eff_ghz": f_eff,
+            "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
+            "kernel": st["dom_kernel"],
+            "launches_per_step": launches,
+            "avg_launch_ms": round(avg_ms, 3),
+            "nonces_per_launch": int(nonces_pl),
+            "ops_per_nonce": round(OPS_PER_COMPRESSION * C_eff, 3),
+            "valu_instr_per_nonce_pmc": round(valu_pmc, 1) if valu_pmc else None,
+            # executed lane-ops (PMC VALU instructions x 64 lanes per 64
+            # nonces) / peak: the issue-level fraction (DESIGN §4)
+            "executed_frac": round(valu_pmc * st["dom_nonces"]
+                                   / (st["dom_kernel_ms"] * 1e-3) / 1e12
+                                   / PEAK_TOPS, 4) if valu_pmc else None,
+            "kernel_GHs": round(st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary cfg3 measurement of the default cfg2 run")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
     args = ap.parse_args()
     msg, desc = WORKLOADS[args.workload]
@@ -165,6 +237,55 @@ def main():
             dist.init_process_group(backend, rank=rank, world_size=world)
 
     ctx = _lib.Context([gpu])
+    # HM_BENCH_STREAMS=1: strictly serial launches (kernel traces then
+    # attribute time without cross-stream queue waits)
+    if os.environ.get("HM_BENCH_STREAMS"):
+        ctx.set_option(_lib.HM_OPT_STREAMS, int(os.environ["HM_BENCH_STREAMS"]))
+    dev = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
+    cdev = torch.device("cuda", gpu)
+    cand = torch.empty(2, dtype=torch.int64, device=dev)
+    gathered = torch.empty(2 * world, dtype=torch.int64, device=dev)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(cdev)
+
+    def measure(m, lo, hi, steps, warmup):
+        """W untimed + K timed steps of (this rank's hm_scan, all-gather of
+        the 16-B candidates, min); returns (max-over-ranks seconds, result,
+        rank-0 step times, hm_stats of the last scan)."""
+        def step():
+            local = ctx.scan(m, lo, hi)
+            if dist is None:
+                return local
+            cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
+            dist.all_gather_into_tensor(gathered, cand)  # 16 B per rank over RCCL
+            arr = gathered.cpu().numpy().view(np.uint64).reshape(world, 2)
+            return merge((int(a), int(b)) for a, b in arr)
+
+        res = None
+        for _ in range(warmup):
+            res = step()
+        barrier()
+        t0 = time.perf_counter()
+        step_ms = []
+        for _ in range(steps):
+            ts = time.perf_counter()
+            res = step()  # hm_scan returns after its 16-B readback: the step is complete
+            step_ms.append((time.perf_counter() - ts) * 1e3)
+        torch.cuda.synchronize(cdev)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        st = ctx.stats()
+        if dist is not None:
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        # self-check: the winner re-hashes to the reported hash (host hm_hash)
+        assert _lib.host_hash(m, res[1]) == res[0], res
+        return elapsed, res, step_ms, st
+
     if args.workload == "cfg4":
         from distributed_bitcoinminer_amd.parallel import shard_range
         total_nonces = 1 << 40
@@ -172,64 +293,28 @@ def main():
     else:
         total_nonces = world * PER_GPU
         lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1
-    dev = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
-    cdev = torch.device("cuda", gpu)
-    cand = torch.empty(2, dtype=torch.int64, device=dev)
-    gathered = torch.empty(2 * world, dtype=torch.int64, device=dev)
+    elapsed, res, step_ms, st = measure(msg, lo, hi, args.steps, args.warmup)
+    rl = roofline(st, msg, lo, hi) if rank == 0 else None
 
-    def step():
-        local = ctx.scan(msg, lo, hi)
-        if dist is None:
-            return local
-        cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
-        dist.all_gather_into_tensor(gathered, cand)  # 16 B per rank over RCCL
-        arr = gathered.cpu().numpy().view(np.uint64).reshape(world, 2)
-        return merge((int(a), int(b)) for a, b in arr)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(cdev)
-
-    for _ in range(args.warmup):
-        res = step()
-    barrier()
-    t0 = time.perf_counter()
-    step_ms = []
-    for _ in range(args.steps):
-        ts = time.perf_counter()
-        res = step()  # hm_scan returns after its 16-B readback: the step is complete
-        step_ms.append((time.perf_counter() - ts) * 1e3)
-    torch.cuda.synchronize(cdev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    st = ctx.stats()
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-
-    # self-check: the winner re-hashes to the reported hash (host hm_hash)
-    assert _lib.host_hash(msg, res[1]) == res[0], res
+    # secondary: BASELINE configs[2] (120-B message, two tail blocks), same
+    # weak-scaling shards, so the driver's run times config 3 as well
+    secondary = None
+    if args.workload == "cfg2" and not args.no_secondary:
+        m3 = long120()
+        steps3 = max(1, min(args.steps, 5))
+        e3, r3, sm3, st3 = measure(m3, lo, hi, steps3, 1)
+        if rank == 0:
+            secondary = {"cfg3": {
+                "workload": WORKLOADS["cfg3"][1], "value": round(total_nonces * steps3 / e3 / 1e9, 3),
+                "unit": "GH/s", "steps": steps3, "warmup": 1,
+                "ms_per_step": round(e3 / steps3 * 1e3, 3),
+                "ms_per_step_median_rank0": round(sorted(sm3)[len(sm3) // 2], 3),
+                "result": {"hash": r3[0], "nonce": r3[1]},
+                "roofline": roofline(st3, m3, lo, hi)}}
 
     if rank == 0:
         total = total_nonces * args.steps
         value = total / elapsed / 1e9
-        C = st["dom_compressions"]
-        # per launch: algorithmic ops / average launch duration of the dominant kernel
-        launches = max(1, st["dom_launches"])
-        avg_ms = st["dom_kernel_ms"] / launches
-        ops_per_launch = st["dom_nonces"] / launches * OPS_PER_COMPRESSION * C
-        achieved = ops_per_launch / (avg_ms * 1e-3) / 1e12
-        traffic, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
-        # algorithmic HBM bytes of one dominant launch: its 128-B tile records
-        # (10^V nonces each) + one 16-B candidate per wave of the grid; the
-        # work queue adds one device-scope atomicAdd per dequeued task
-        dom_seg = max(_lib.debug_plan(msg, lo, hi), key=lambda s: s["hi"] - s["lo"])
-        nonces_pl = st["dom_nonces"] // launches
-        tiles_pl = -(-nonces_pl // 10 ** dom_seg["V"])
-        algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
-        tasks_pl = nonces_pl // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
         line = {
             "metric": "GH/s (SHA-256 nonce search) at 1/2/4/8 MI355X; % of INT32 VALU roofline",
             "value": round(value, 3),
@@ -249,35 +334,10 @@ def main():
                        "merge": ("RCCL all-gather" if backend == "nccl" else backend)
                                 if dist is not None else "none (1 rank)"},
             "result": {"hash": res[0], "nonce": res[1]},
-            "roofline": {"bound": "valu", "achieved": round(achieved, 3),
-                         "peak": round(PEAK_TOPS, 3), "unit": "T int32 lane-ops/s",
-                         "frac": round(achieved / PEAK_TOPS, 4), "traffic": traffic,
-                         "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                         "traffic_source": traffic_src,
-                         "algorithmic_bytes_per_launch": algo_bytes,
-                         "queue_atomics_per_launch": tasks_pl,
-                         "traffic_note": "PMC traffic is the work queue's device-scope atomics "
-                                         "(one per dequeued task, executed memory-side), not "
-                                         "re-reads; cutting them 4x cut WRITE_SIZE 4x but cost "
-                                         "kernel rate (DESIGN.md §9)",
-                         "f_eff_ghz": f_eff,
-                         "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
-                         "kernel": st["dom_kernel"],
-                         "launches_per_step": launches,
-                         "avg_launch_ms": round(avg_ms, 3),
-                         "nonces_per_launch": st["dom_nonces"] // launches,
-                         "ops_per_nonce": OPS_PER_COMPRESSION * C,
-                         "valu_instr_per_nonce_pmc": round(valu_pmc, 1) if valu_pmc else None,
-                         # executed lane-ops (PMC VALU instructions x 64 lanes per
-                         # 64 nonces) / peak: the issue-level fraction. The
-                         # nominal `frac` prices 1552*C ops per nonce and exceeds
-                         # 1 for the chained kernel, whose wave-uniform final
-                         # block needs no per-lane message schedule
-                         "executed_frac": round(valu_pmc * st["dom_nonces"]
-                                                / (st["dom_kernel_ms"] * 1e-3) / 1e12
-                                                / PEAK_TOPS, 4) if valu_pmc else None,
-                         "kernel_GHs": round(st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9, 3)},
+            "roofline": rl,
         }
+        if secondary:
+            line["workloads"] = secondary
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(msg, args.workload)
             line["cpu_baseline"] = cb

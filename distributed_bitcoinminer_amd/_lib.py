@@ -25,6 +25,7 @@ HM_ERR_INTERNAL = -6
 
 HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
+HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
 class HipMinerError(RuntimeError):
@@ -49,11 +50,11 @@ class hm_stats(ctypes.Structure):
                 ("dom_nonces", ctypes.c_uint64), ("dom_compressions", ctypes.c_uint64),
                 ("launches", ctypes.c_int32), ("dom_kind", ctypes.c_int32),
                 ("ndev", ctypes.c_int32), ("dom_grid", ctypes.c_int32),
-                ("dom_launches", ctypes.c_int32), ("reserved", ctypes.c_int32),
-                ("dom_kernel", ctypes.c_char * 64)]
+                ("dom_launches", ctypes.c_int32), ("merge", ctypes.c_int32),
+                ("dom_kernel", ctypes.c_char * 64), ("dom_compressions_eff", ctypes.c_double)]
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
         d["dom_kernel"] = self.dom_kernel.decode()
         return d
 

@@ -63,6 +63,7 @@ struct Launch {
     int kind;
     int grid;
     uint32_t compressions;
+    double comp_eff;  // compressions per nonce the kernel executes (hm_stats)
     char kernel[64];  // kernel instantiation, as rocprofv3 names it (sans args)
 };
 
@@ -116,7 +117,7 @@ int hip_fail(hipError_t e, const char* what) {
 }  // namespace
 
 struct hm_ctx {
-    std::mutex mu;
+    mutable std::mutex mu;
     std::vector<Device> devs;
     bool force_generic = false;
     bool merge_rccl = false;
@@ -124,6 +125,7 @@ struct hm_ctx {
     int streams = kStreams;  // HM_OPT_STREAMS (tail filling by default)
     bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
     bool have_stats = false;
+    int merge = HM_MERGE_NONE;  // how the current call merged device results
     hm_stats last{};
 };
 
@@ -246,6 +248,19 @@ uint32_t count_compressions(const SegPlan& s) {
     return s.nb;
 }
 
+// Compressions per nonce the segment's scan kernel executes: the algorithmic
+// C minus what is hoisted out of the per-nonce loop (hm_stats.dom_compressions_eff).
+double executed_compressions(const SegPlan& s) {
+    switch (s.kind) {
+        case HM_KIND_TILED:  // a two-block tail's block 0 is compressed per tile by the planner
+            return s.trailer ? 2.0 : 1.0;
+        case HM_KIND_CHAINED:  // per-lane block 0 once per loop chunk of tch values
+            return 1.0 + 1.0 / (double)s.tch;
+        default:
+            return (double)s.nb;
+    }
+}
+
 int persistent_grid(const hm_ctx* ctx, const Device& dv, int per_cu_auto, uint64_t ntasks) {
     int per_cu = ctx->grid_per_cu > 0 ? ctx->grid_per_cu : per_cu_auto;
     if (per_cu <= 0) per_cu = 1;
@@ -355,6 +370,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
         L.grid = grid;
         L.compressions = count_compressions(s);
+        L.comp_eff = executed_compressions(s);
         HIPCHK(hipEventRecord(L.start, st));
         rc = launch_scan(*fn, ca, grid, st);
         if (rc) return rc;
@@ -434,6 +450,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             name_tiled(L.kernel, s, ctx->csum);
             L.grid = grid;
             L.compressions = count_compressions(s);
+            L.comp_eff = executed_compressions(s);
             HIPCHK(hipEventRecord(L.start, st));
             rc = launch_scan(*fn, ta, grid, st);
             if (rc) return rc;
@@ -477,6 +494,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_generic_csum_kernel" : "hm_generic_kernel");
     L.grid = grid;
     L.compressions = count_compressions(s);
+    L.comp_eff = executed_compressions(s);
     HIPCHK(hipEventRecord(L.start, st));
     rc = launch_scan(*fn, ga, grid, st);
     if (rc) return rc;
@@ -497,11 +515,13 @@ struct DevReq {
 
 // Enqueue a batch of scans on one device; request r's result lands in
 // dv.result + 2r.  All segments of all requests are queued before any sync.
-int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& reqs) {
+// `first`: the call's first chunk, which records the timing origin dv.t0
+// (every launch of an hm_scan_many call is timed against it).
+int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& reqs, bool first) {
     HIPCHK(hipSetDevice(dv.ordinal));
     const int n = (int)reqs.size();
     hipStream_t s0 = dv.stream[0];
-    HIPCHK(hipEventRecord(dv.t0, s0));
+    if (first) HIPCHK(hipEventRecord(dv.t0, s0));
     HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
     HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
     if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
@@ -572,8 +592,13 @@ bool lex_less(uint64_t k1, uint64_t n1, uint64_t k2, uint64_t n2) {
 }
 
 // All-gather every device's n 16-B results over RCCL; device 0 folds them.
+// Runs for any device count, including one (a 1-rank communicator), so the
+// path the 8-GPU context takes is exercised on a 1-GPU box.
 int rccl_merge(hm_ctx* ctx, int nreq) {
     const int n = (int)ctx->devs.size();
+    for (int i = 0; i < n; ++i)  // one RCCL rank per device: ordinals must differ
+        for (int j = 0; j < i; ++j)
+            if (ctx->devs[i].ordinal == ctx->devs[j].ordinal) return HM_ERR_INVALID;
     if (!ctx->devs[0].comm) {
         std::vector<ncclComm_t> comms(n);
         std::vector<int> ords(n);
@@ -607,7 +632,7 @@ int rccl_merge(hm_ctx* ctx, int nreq) {
 }
 
 // One chunk (<= kMaxBatch requests) of hm_scan_many.
-int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
+int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, bool first) {
     const int ndev = (int)ctx->devs.size();
     std::vector<MsgPlan> plans(nreq);
     std::vector<std::vector<DevReq>> per_dev(ndev, std::vector<DevReq>(nreq));
@@ -627,12 +652,13 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
         }
     }
     for (int i = 0; i < ndev; ++i) {
-        int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i]);
+        int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i], first);
         if (rc) return rc;
     }
-    if (ndev > 1 && ctx->merge_rccl) {
+    if (ctx->merge_rccl) {
         int rc = rccl_merge(ctx, nreq);
         if (rc) return rc;
+        ctx->merge = HM_MERGE_RCCL;
         Device& d0 = ctx->devs[0];
         HIPCHK(hipSetDevice(d0.ordinal));
         HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, nreq * sizeof(hm_result),
@@ -644,6 +670,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs) {
         for (int r = 0; r < nreq; ++r) outs[r] = d0.host_out[r];
         return HM_OK;
     }
+    ctx->merge = ndev > 1 ? HM_MERGE_HOST : HM_MERGE_NONE;
     for (auto& dv : ctx->devs) {
         HIPCHK(hipSetDevice(dv.ordinal));
         HIPCHK(hipMemcpyAsync(dv.host_out, dv.result, nreq * sizeof(hm_result),
@@ -671,8 +698,9 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
     return host_hash(msg ? msg : &empty, msg ? len : 0, nonce);
 }
 
-// 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked
-int hm_version(void) { return (1 << 16) | 3; }
+// 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked;
+// 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count
+int hm_version(void) { return (1 << 16) | 4; }
 
 int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t* bounds) {
@@ -788,9 +816,10 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
     uint64_t total = 0;
     for (int r = 0; r < n; ++r)
         if (reqs[r].lo <= reqs[r].hi) total += reqs[r].hi - reqs[r].lo + 1;  // wraps for 2^64
+    ctx->merge = HM_MERGE_NONE;
     for (int c = 0; c < n; c += kMaxBatch) {
         const int m = std::min(kMaxBatch, n - c);
-        int rc = scan_chunk(ctx, reqs + c, m, res.data() + c);
+        int rc = scan_chunk(ctx, reqs + c, m, res.data() + c, c == 0);
         if (rc) return rc;
     }
     const int ndev = (int)ctx->devs.size();
@@ -800,7 +829,8 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
     st.nonces = total;
     // aggregate per kernel instantiation; the dominant one has the most nonces
     struct Agg { std::string name; double ms = 0; uint64_t nonces = 0; int launches = 0;
-                 int kind = 0, grid = 0; uint32_t comp = 0; uint64_t big = 0; };
+                 int kind = 0, grid = 0; uint32_t comp = 0; double comp_eff = 0;
+                 uint64_t big = 0; };
     std::vector<Agg> aggs;
     for (auto& dv : ctx->devs) {
         // kernel_ms: time during which some scan kernel ran on this device
@@ -838,6 +868,7 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
             a->launches += 1;
             a->kind = L.kind;
             a->comp = std::max(a->comp, L.compressions);
+            a->comp_eff += L.comp_eff * (double)L.nonces;  // nonce-weighted mean below
             if (L.nonces > a->big) { a->big = L.nonces; a->grid = L.grid; }
         }
     }
@@ -846,12 +877,14 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
             st.dom_nonces = a.nonces;
             st.dom_kernel_ms = a.ms;
             st.dom_compressions = a.comp;
+            st.dom_compressions_eff = a.nonces ? a.comp_eff / (double)a.nonces : 0.0;
             st.dom_kind = a.kind;
             st.dom_grid = a.grid;
             st.dom_launches = a.launches;
             snprintf(st.dom_kernel, sizeof st.dom_kernel, "%s", a.name.c_str());
         }
     }
+    st.merge = ctx->merge;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
                      .count();
     ctx->last = st;
@@ -904,7 +937,9 @@ int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, ui
 
 
 int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
-    if (!ctx || !out || !ctx->have_stats) return HM_ERR_INVALID;
+    if (!ctx || !out) return HM_ERR_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);  // scans write ctx->last under the lock
+    if (!ctx->have_stats) return HM_ERR_INVALID;
     *out = ctx->last;
     return HM_OK;
 }

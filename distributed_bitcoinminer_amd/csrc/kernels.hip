@@ -25,18 +25,8 @@ __global__ void __launch_bounds__(kBlock) hm_tile_plan_kernel(const PlanArgs A) 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.ntiles) return;
     uint32_t w[32];
-#pragma unroll
-    for (int k = 0; k < 32; ++k) w[k] = k < 16 ? A.pw[k] : 0u;
-    uint64_t x = (A.tile0 + i) * A.pow10V;  // tile base: low V digits are zero
-    for (int j = (int)A.d - 1; j >= 0; --j) {
-        const uint64_t y = x / 10u;
-        const uint32_t dig = (uint32_t)(x - y * 10u);
-        x = y;
-        if ((uint32_t)j < A.d - A.V) put_byte(w, A.r + (uint32_t)j, 0x30u + dig);
-    }
-    put_byte(w, A.r + A.d, 0x80u);
-    w[16 * A.nb - 2] = (uint32_t)(A.total_bits >> 32);
-    w[16 * A.nb - 1] = (uint32_t)A.total_bits;
+    // tile base; its low V digits (varied by the scan kernels) stay zero bytes
+    build_tail(w, A.pw, A.r, A.d, A.V, (A.tile0 + i) * A.pow10V, A.nb, A.total_bits);
     uint32_t st[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) st[k] = A.mid[k];
@@ -58,18 +48,13 @@ __global__ void __launch_bounds__(kBlock) hm_kw_table_kernel(uint32_t* __restric
                                                              uint64_t total_bits) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
+    // f digits of t with leading zeros (t < 10^f), then 0x80 and the length
+    uint32_t b[32];
+    const uint32_t zero[16] = {0};
+    build_tail(b, zero, 0, f, 0, t, 1, total_bits);
     uint32_t w[64];
 #pragma unroll
-    for (int k = 0; k < 64; ++k) w[k] = 0;
-    uint32_t x = t;
-    for (int j = (int)f - 1; j >= 0; --j) {  // f digits with leading zeros
-        const uint32_t y = x / 10u;
-        put_byte(w, (uint32_t)j, 0x30u + x - y * 10u);
-        x = y;
-    }
-    put_byte(w, f, 0x80u);
-    w[14] = (uint32_t)(total_bits >> 32);
-    w[15] = (uint32_t)total_bits;
+    for (int k = 0; k < 64; ++k) w[k] = k < 16 ? b[k] : 0u;
     h_schedule(w);
     uint32_t* o = out + (size_t)t * 64;
 #pragma unroll

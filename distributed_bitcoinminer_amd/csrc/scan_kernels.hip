@@ -289,22 +289,19 @@ DEV void generic_body(const GenericArgs& A) {
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k <= A.count_m1;) {
         const uint64_t n = A.seg_lo + k;
         uint32_t w[32];
-#pragma unroll
-        for (int j = 0; j < 32; ++j) w[j] = j < 16 ? A.pw[j] : 0u;
-        uint64_t x = n;
-        for (int j = (int)A.d - 1; j >= 0; --j) {
-            const uint64_t y = x / 10u;
-            put_byte(w, A.r + (uint32_t)j, 0x30u + (uint32_t)(x - y * 10u));
-            x = y;
-        }
-        put_byte(w, A.r + A.d, 0x80u);
-        w[16 * A.nb - 2] = (uint32_t)(A.total_bits >> 32);
-        w[16 * A.nb - 1] = (uint32_t)A.total_bits;
+        build_tail(w, A.pw, A.r, A.d, 0, n, A.nb, A.total_bits);
         uint32_t st[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) st[j] = A.mid[j];
-        h_compress(st, w);
-        if (A.nb == 2) h_compress(st, w + 16);
+        uint32_t m[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) m[j] = w[j];
+        d_compress(st, m);
+        if (A.nb == 2) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) m[j] = w[16 + j];
+            d_compress(st, m);
+        }
         const uint64_t key = ((uint64_t)st[0] << 32) | st[1];
         if constexpr (CSUM) { csum += key; ++ccnt; }
         if (key < bk || (key == bk && n < bn)) { bk = key; bn = n; }

@@ -34,7 +34,9 @@ static constexpr uint32_t kK[64] = {
 HM_HD uint32_t h_rotr(uint32_t x, uint32_t n) { return (x >> n) | (x << (32u - n)); }
 
 // Message schedule of one block: w[0..15] in, w[0..63] out.
+// (Loops are fully unrolled so that on the device w stays in registers.)
 HM_HD void h_schedule(uint32_t w[64]) {
+#pragma unroll
     for (int i = 16; i < 64; ++i) {
         uint32_t a = w[i - 15], b = w[i - 2];
         uint32_t s0 = h_rotr(a, 7) ^ h_rotr(a, 18) ^ (a >> 3);
@@ -46,10 +48,12 @@ HM_HD void h_schedule(uint32_t w[64]) {
 // One compression, state updated in place (with the feed-forward add).
 HM_HD void h_compress(uint32_t st[8], const uint32_t m[16]) {
     uint32_t w[64];
+#pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = m[i];
     h_schedule(w);
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6],
              h = st[7];
+#pragma unroll
     for (int i = 0; i < 64; ++i) {
         uint32_t t1 = h + (h_rotr(e, 6) ^ h_rotr(e, 11) ^ h_rotr(e, 25)) + (((f ^ g) & e) ^ g) +
                       kK[i] + w[i];

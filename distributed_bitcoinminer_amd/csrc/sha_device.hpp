@@ -116,6 +116,14 @@ DEV void sha_rounds(State& s, uint32_t m[16], uint32_t s0w = 0) {
     rounds_seq<VM, SW>(s, m, s0w, std::make_integer_sequence<int, 64>{});
 }
 
+// One full compression of a lane-varying block (generic kernel): st += rounds(m).
+DEV void d_compress(uint32_t st[8], uint32_t m[16]) {
+    State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+    sha_rounds<0xFFFFu>(s, m);
+    st[0] += s.a; st[1] += s.b; st[2] += s.c; st[3] += s.d;
+    st[4] += s.e; st[5] += s.f; st[6] += s.g; st[7] += s.h;
+}
+
 template <int I>
 DEV void round_kw(State& s, uint32_t kw) {
     // INV_STATE: round 0 of a block whose start state is invariant in the
@@ -143,23 +151,80 @@ DEV void sha_rounds_kw(State& s, KW kw) {
 // the compiler reads it with scalar loads (SGPR operands, no VMEM in the loop).
 typedef const __attribute__((address_space(4))) uint32_t const_u32;
 
+// Cross-lane exchange without LDS (gfx950).  Each step gives every lane a
+// second value so that, after the six steps of a reduction, every lane has
+// seen all 64: DPP within rows of 16 (quad_perm [1,0,3,2] and [2,3,0,1], then
+// row_half_mirror and row_mirror, which reach the other quad / half-row once
+// those hold equal values), v_permlane16_swap across row pairs and
+// v_permlane32_swap across the wave halves.  A swap of x with itself returns
+// (x from one side, x from the other) for a lane pair, i.e. both operands of
+// the pair's combine, on both lanes.
+template <int CTRL> DEV uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL> DEV uint64_t dpp64(uint64_t x) {
+    return ((uint64_t)dpp32<CTRL>((uint32_t)(x >> 32)) << 32) | dpp32<CTRL>((uint32_t)x);
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // row_half_mirror: lane i <-> 7-i within 8
+constexpr int kDppMirror = 0x140;     // row_mirror: lane i <-> 15-i within 16
+
+// permlane{16,32}_swap of a 64-bit value with itself: (side A, side B).
+template <int W> DEV void swap64(uint64_t x, uint64_t& a, uint64_t& b) {
+    const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+    if constexpr (W == 16) {
+        const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+        const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+        a = ((uint64_t)h[0] << 32) | l[0];
+        b = ((uint64_t)h[1] << 32) | l[1];
+    } else {
+        const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+        const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+        a = ((uint64_t)h[0] << 32) | l[0];
+        b = ((uint64_t)h[1] << 32) | l[1];
+    }
+}
+
+DEV void lex_take(uint64_t& k, uint64_t& n, uint64_t k2, uint64_t n2) {
+    const bool take = (k2 < k) || (k2 == k && n2 < n);
+    k = take ? k2 : k;
+    n = take ? n2 : n;
+}
+
+template <int CTRL> DEV void min_step_dpp(uint64_t& k, uint64_t& n) {
+    lex_take(k, n, dpp64<CTRL>(k), dpp64<CTRL>(n));
+}
+template <int W> DEV void min_step_swap(uint64_t& k, uint64_t& n) {
+    uint64_t ka, kb, na, nb;
+    swap64<W>(k, ka, kb);
+    swap64<W>(n, na, nb);
+    k = ka;
+    n = na;
+    lex_take(k, n, kb, nb);
+}
+
 // Lexicographic (key, nonce) min across the 64 lanes; every lane gets it.
 DEV void wave_min(uint64_t& k, uint64_t& n) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t k2 = __shfl_xor(k, off, kWaveSize);
-        const uint64_t n2 = __shfl_xor(n, off, kWaveSize);
-        const bool take = (k2 < k) || (k2 == k && n2 < n);
-        k = take ? k2 : k;
-        n = take ? n2 : n;
-    }
+    min_step_dpp<kDppXor1>(k, n);
+    min_step_dpp<kDppXor2>(k, n);
+    min_step_dpp<kDppHalfMirror>(k, n);
+    min_step_dpp<kDppMirror>(k, n);
+    min_step_swap<16>(k, n);
+    min_step_swap<32>(k, n);
 }
 
 // Wrapping sum across the 64 lanes; every lane gets it.
 DEV uint64_t wave_sum(uint64_t x) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, kWaveSize);
-    return x;
+    x += dpp64<kDppXor1>(x);
+    x += dpp64<kDppXor2>(x);
+    x += dpp64<kDppHalfMirror>(x);
+    x += dpp64<kDppMirror>(x);
+    uint64_t a, b;
+    swap64<16>(x, a, b);
+    x = a + b;
+    swap64<32>(x, a, b);
+    return a + b;
 }
 
 // Checked scans: lane 0 stores the wave's (sum of keys, count) coverage pair.
@@ -172,8 +237,58 @@ DEV void store_sums(uint64_t* sums, uint32_t wslot, uint64_t sum, uint64_t cnt) 
     }
 }
 
-DEV void put_byte(uint32_t* w, uint32_t pos, uint32_t byte) {
-    w[pos >> 2] |= byte << (24u - 8u * (pos & 3u));
+// Tail block words of msg ‖ ' ' ‖ decimal(n) after the midstate (hash.go:15):
+// r prefix bytes (pw, zero past r), the d digits of n, 0x80, zeros and the
+// 64-bit bit length in the last two words of block nb-1.  The `skip` lowest
+// digits are left as zero bytes (the tile planner's varying digits).
+// Every array index is a compile-time constant after unrolling, so w and the
+// digit words stay in registers (no scratch).  Digit positions are taken
+// relative to E = r + d - 1 (wave-uniform): the k-th least significant digit
+// lands in word kE - k/4 or the one below, so the digits and 0x80 fill a
+// 7-word window (words kE - 5 .. kE + 1), which a 5-stage barrel shift by
+// the uniform kE moves into place -- 5 uniform conditions instead of a
+// compare per (word, window slot), which would all be loop-invariant SGPR
+// masks.
+DEV void build_tail(uint32_t w[32], const uint32_t* pw, uint32_t r, uint32_t d, uint32_t skip,
+                    uint64_t n, uint32_t nb, uint64_t total_bits) {
+    const uint32_t E = r + d - 1, kE = E >> 2, e = E & 3u;
+    // before the shift v[i] holds word i - 5 + kE of the window (i in [0, 6]:
+    // words kE - 5 .. kE + 1); after it v[5 + k] holds word k
+    uint32_t v[37];
+#pragma unroll
+    for (int i = 0; i < 37; ++i) v[i] = 0u;
+    uint64_t x = n;
+#pragma unroll
+    for (uint32_t k = 0; k < 20; ++k) {
+        if (k < d) {
+            const uint64_t y = x / 10u;
+            const uint32_t b = k < skip ? 0u : (0x30u + (uint32_t)(x - y * 10u))
+                                                   << (24u - 8u * ((e - k) & 3u));
+            x = y;
+            const bool below = (k & 3u) > e;  // crosses into the next lower word
+            v[5 - (k >> 2)] |= below ? 0u : b;
+            v[4 - (k >> 2)] |= below ? b : 0u;
+        }
+    }
+    if (e == 3u) v[6] = 0x80u << 24;
+    else v[5] |= 0x80u << (16u - 8u * e);
+    // shift left by kE words: afterwards v[5 + k] = word k (k in [0, 31])
+#pragma unroll
+    for (int b = 1; b <= 16; b <<= 1) {
+        const bool on = (kE & (uint32_t)b) != 0;
+#pragma unroll
+        for (int i = 36; i >= 0; --i) v[i] = on ? (i >= b ? v[i - b] : 0u) : v[i];
+    }
+    const bool two = nb == 2;
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+        uint32_t o = (k < 16 ? pw[k] : 0u) | v[5 + k];
+        if (k == 14) o = two ? o : (uint32_t)(total_bits >> 32);
+        if (k == 15) o = two ? o : (uint32_t)total_bits;
+        if (k == 30) o = two ? (uint32_t)(total_bits >> 32) : o;
+        if (k == 31) o = two ? (uint32_t)total_bits : o;
+        w[k] = o;
+    }
 }
 
 }  // namespace hm

@@ -77,9 +77,25 @@ typedef struct hm_stats {
     int32_t ndev;            /* devices used                                      */
     int32_t dom_grid;        /* workgroups of the dominant kernel's largest launch */
     int32_t dom_launches;    /* launches of the dominant kernel                  */
-    int32_t reserved;
+    int32_t merge;           /* HM_MERGE_*: how the per-device 16-B results were
+                                merged (ABI 1.4; was reserved)                   */
     char dom_kernel[64];     /* its name as rocprofv3 lists it (without args)   */
+    double dom_compressions_eff; /* SHA-256 compressions per nonce the dominant
+                                  kernel executes (ABI 1.4): dom_compressions
+                                  minus the work hoisted out of the per-nonce
+                                  loop.  Tiled: 1 (+1 with a constant trailer
+                                  block); chained: 1 + 1/tch, the per-lane block
+                                  0 amortised over tch = min(10^f, 1000) loop
+                                  values; generic: dom_compressions.  Mean
+                                  over the dominant kernel's nonces (one
+                                  instantiation may serve several segments). */
 } hm_stats;
+
+#define HM_MERGE_NONE 0 /* one device: its result is read back directly      */
+#define HM_MERGE_HOST 1 /* several devices: 16-B results merged on the host  */
+#define HM_MERGE_RCCL 2 /* RCCL ncclAllGather of the 16-B results on the
+                           devices, then a device-side lexicographic fold
+                           (HM_OPT_MERGE_RCCL; any device count, incl. 1)    */
 
 #define HM_OK 0
 #define HM_ERR_INVALID (-1)   /* bad argument                                   */
@@ -96,7 +112,10 @@ typedef struct hm_stats {
 
 /* Options for hm_set_option. */
 #define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */
-#define HM_OPT_MERGE_RCCL 2    /* 1: merge multi-device candidates with RCCL     */
+#define HM_OPT_MERGE_RCCL 2    /* 1: merge the per-device candidates with one RCCL
+                                  all-gather (also with one device: a 1-rank
+                                  communicator); needs distinct device ordinals,
+                                  else hm_scan* return HM_ERR_INVALID         */
 #define HM_OPT_GRID_PER_CU 3   /* workgroups per CU for scan launches (0 = auto) */
 #define HM_OPT_STREAMS 4       /* HIP streams per device for segment launches
                                   (1..4, default 4): the dominant kernel's

@@ -14,6 +14,12 @@ Two independent restatements of the reference hot path live here
   liboracle.so`` (``oracle/hm_oracle.c``: its own FIPS 180-4 SHA-256 and the
   Sprintf formatting), multi-threaded; used for larger parity ranges and as
   the CPU baseline in bench.py.
+* ``fast_scan_sum``: ctypes over ``oracle/build/liboracle_fast.so``
+  (``oracle/hm_oracle_fast.c``): the same scan with a per-segment midstate,
+  in-place ASCII digit increments and the x86 SHA extensions.  Used only in
+  the build container to generate the full-size fixtures (2^40 nonces of
+  config 4, config 5's 20-digit ranges); checked against ``c_scan_sum`` by
+  ``tests/test_oracle_fast.py``.
 """
 from __future__ import annotations
 
@@ -25,7 +31,9 @@ import subprocess
 MAXU64 = (1 << 64) - 1
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_FAST_PATH = os.path.join(_HERE, "build", "liboracle_fast.so")
 _lib = None
+_fast = None
 
 
 def build() -> str:
@@ -141,3 +149,39 @@ def c_miner_eval(msg, lower: int, upper: int, threads: int = 0):
     h, n = ctypes.c_uint64(), ctypes.c_uint64()
     _load().oracle_miner_eval(m, len(m), lower, upper, threads, ctypes.byref(h), ctypes.byref(n))
     return int(h.value), int(n.value)
+
+
+# ---- fast C restatement (SHA extensions; fixture generation) ----------------
+
+def _load_fast():
+    global _fast
+    if _fast is None:
+        if not os.path.exists(_FAST_PATH):
+            build()
+        lib = ctypes.CDLL(_FAST_PATH)
+        lib.oracle_fast_available.restype = ctypes.c_int
+        lib.oracle_fast_available.argtypes = []
+        lib.oracle_fast_scan_sum.restype = None
+        lib.oracle_fast_scan_sum.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64,
+                                             ctypes.c_uint64, ctypes.c_int] + \
+            [ctypes.POINTER(ctypes.c_uint64)] * 4
+        _fast = lib
+    return _fast
+
+
+def fast_available() -> bool:
+    """True when this CPU has the SHA extensions hm_oracle_fast.c needs."""
+    return bool(_load_fast().oracle_fast_available())
+
+
+def fast_scan_sum(msg, lo: int, hi: int, threads: int = 0):
+    """c_scan_sum's contract, computed by oracle/hm_oracle_fast.c."""
+    if not fast_available():
+        raise RuntimeError("CPU lacks the SHA extensions (hm_oracle_fast.c)")
+    m = _b(msg)
+    if threads <= 0:
+        threads = os.cpu_count() or 1
+    h, n, s, c = (ctypes.c_uint64() for _ in range(4))
+    _load_fast().oracle_fast_scan_sum(m, len(m), lo, hi, threads, ctypes.byref(h), ctypes.byref(n),
+                                      ctypes.byref(s), ctypes.byref(c))
+    return (int(h.value), int(n.value)), int(s.value), int(c.value)

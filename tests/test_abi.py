@@ -25,7 +25,7 @@ def test_library_is_gfx950_code_object():
 def test_version_and_strerror():
     lib = _lib.load()
     assert lib.hm_version() >> 16 == 1
-    assert lib.hm_version() & 0xFFFF >= 3  # 1.3: hm_scan_checked
+    assert lib.hm_version() & 0xFFFF >= 4  # 1.4: hm_stats.merge / dom_compressions_eff
     for rc in range(0, -7, -1):
         assert _lib.strerror(rc)
     assert _lib.strerror(-99) == "unknown error"
@@ -53,3 +53,24 @@ def test_open_without_gpu_fails_loudly():
     with pytest.raises(_lib.HipMinerError) as ei:
         _lib.Context([0])
     assert ei.value.rc == _lib.HM_ERR_NO_DEVICE
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors of hm_stats / hm_request / hm_result have the C
+    layout (size and every field offset) that include/hipminer.h gives."""
+    import subprocess
+    fields = [f for f, _ in _lib.hm_stats._fields_]
+    src = tmp_path / "layout.c"
+    lines = ['#include <stddef.h>', '#include <stdio.h>', f'#include "{_lib.HEADER_PATH}"',
+             "int main(void) {",
+             '  printf("%zu %zu %zu\\n", sizeof(hm_stats), sizeof(hm_request), sizeof(hm_result));']
+    lines += [f'  printf("%zu\\n", offsetof(hm_stats, {f}));' for f in fields]
+    lines += ["  return 0;", "}"]
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    sizes = [int(x) for x in out[:3]]
+    assert sizes == [ctypes.sizeof(_lib.hm_stats), ctypes.sizeof(_lib.hm_request),
+                     ctypes.sizeof(_lib.hm_result)]
+    assert [int(x) for x in out[3:]] == [getattr(_lib.hm_stats, f).offset for f in fields]

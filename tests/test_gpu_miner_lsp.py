@@ -99,38 +99,42 @@ def test_three_miners_under_server_model(oracle_mod):
                 p.kill()
 
 
-def test_config5_eight_miners_near_max(oracle_mod):
-    """Config 5 shape: 8 GPU miner processes, the four SURVEY messages as queued
-    client requests near 2^64-1 (20-digit nonces).  Each request is split as
-    server.go:165-205 splits it; the merged answer must equal the A-inv-7
-    model computed with direct scans of the same chunks."""
-    import random
-    from distributed_bitcoinminer_amd import _lib, miner
-    rng = random.Random(440)
-    long120 = bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
-    msgs = [b"bradfitz", b"thom yorke", long120, b"jonny greenwood"]
+def test_config5_eight_miners_near_max():
+    """Config 5 at the SURVEY width: 8 GPU miner processes, the four SURVEY
+    messages as queued client requests [2^64-1-2^34, 2^64-2] (20-digit
+    nonces).  Each request is split as server.go:165-205 splits it; every
+    miner's Result and the merged answer (server.go:273-276) must equal the
+    oracle's (tests/golden/full_size.json, tests/golden/gen_full.py)."""
+    import json
+    from distributed_bitcoinminer_amd import _lib
+    with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+        cases = json.load(f)["cfg5"]
+    assert len(cases) == 4
     srv = H.FakeLspServer(epoch_ms=100, epoch_limit=100)
     procs = [_spawn(srv) for _ in range(8)]
     try:
         cids = [srv.accept(timeout=180) for _ in procs]
         for c in cids:
             assert srv.read(c, timeout=120) == bitcoin.marshal(bitcoin.NewJoin())
-        with _lib.Context([0]) as ctx:
-            direct = miner.Miner(ctx=ctx)
-            for data in msgs:                 # FIFO: one client request at a time
-                lo, up = MAX - 1 - (1 << 30), MAX - 1
-                chunks = sm.load_balance(lo, up, len(cids))
-                assert len(chunks) == 8 and chunks[-1][1] == MAX
-                for c, (a, b) in zip(cids, chunks):
-                    srv.write(c, bitcoin.marshal(bitcoin.NewRequest(data, a, b)))
-                got = []
-                for c in cids:
-                    r, _ = bitcoin.unmarshal(srv.read(c, timeout=300))
-                    got.append((r.Hash, r.Nonce))
-                assert got[-1] == (MAX, 0)        # the chunk ending at 2^64-1 scans nothing
-                exp = sm.expected_client_result(data, lo, up, 8, direct.scan)
-                assert sm.merge_in_arrival_order(got) == exp
-                assert _lib.host_hash(data, exp[1]) == exp[0]
+        for case in cases:                    # FIFO: one client request at a time
+            data = bytes.fromhex(case["msg_hex"])
+            lo, up = int(case["lower"]), int(case["upper"])
+            assert (lo, up) == (MAX - 1 - (1 << 34), MAX - 1)
+            chunks = sm.load_balance(lo, up, len(cids))
+            assert [(int(c["lo"]), int(c["hi"])) for c in case["chunks"]] == chunks
+            assert chunks[-1][1] == MAX
+            for c, (a, b) in zip(cids, chunks):
+                srv.write(c, bitcoin.marshal(bitcoin.NewRequest(data, a, b)))
+            got = []
+            for c in cids:
+                r, _ = bitcoin.unmarshal(srv.read(c, timeout=300))
+                got.append((r.Hash, r.Nonce))
+            exp = [(int(c["hash"]), int(c["nonce"])) for c in case["chunks"]]
+            assert got == exp, case["name"]   # exp[-1] == (MAX, 0): the wrap (miner.go:52)
+            res = case["client_result"]
+            merged = sm.merge_in_arrival_order(got)
+            assert merged == (int(res["hash"]), int(res["nonce"]))
+            assert _lib.host_hash(data, merged[1]) == merged[0]
     finally:
         srv.close()
         for p in procs:

@@ -137,19 +137,50 @@ def test_generic_vs_tiled_large(ctx):
 
 
 def test_options_streams_and_rccl_merge(oracle_mod):
-    """Multi-stream segment overlap and the RCCL candidate merge (1-device
-    communicator on this box) give the same answer as the default path."""
+    """Multi-stream segment overlap and the in-library RCCL merge of the 16-B
+    per-device results (ncclCommInitAll + grouped ncclAllGather + the strided
+    device-side fold over the gathered candidates, api.cpp rccl_merge) give
+    the same answers as the oracle.  On this 1-GPU box the communicator has
+    one rank; the merge path is the one an 8-device context takes, and
+    hm_stats.merge records that it ran (server.go:273-276 merge semantics)."""
     lo, hi = 10**8 - 3_000_000, 10**8 + 3_000_000  # 8- and 9-digit segments
     exp = oracle_mod.c_scan(b"jonny greenwood", lo, hi)
+    rng = random.Random(808)
+    reqs = []
+    for i in range(150):  # > kMaxBatch = 64: three batch chunks, strided fold per request
+        L = rng.randrange(0, 130)
+        m = bytes(rng.randrange(256) for _ in range(L))
+        a = max(0, 10**rng.randrange(1, 20) - rng.randrange(0, 3000))
+        reqs.append((m, a, a + rng.randrange(-3, 5000)))
+    exp_many = [oracle_mod.c_scan(m, a, b) for m, a, b in reqs]
+    ck_lo, ck_hi = 10**9 - 700_000, 10**9 + 500_000
+    exp_ck = oracle_mod.c_scan_sum(b"a" * 45, ck_lo, ck_hi)
     with _lib.Context([0]) as c:
         c.set_option(_lib.HM_OPT_STREAMS, 4)
         assert c.scan(b"jonny greenwood", lo, hi) == exp
+        assert c.stats()["merge"] == _lib.HM_MERGE_NONE
         c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
         assert c.scan(b"jonny greenwood", lo, hi) == exp
+        assert c.stats()["merge"] == _lib.HM_MERGE_RCCL
+        assert c.scan_many(reqs) == exp_many
+        assert c.stats()["merge"] == _lib.HM_MERGE_RCCL
+        assert c.scan_checked(b"a" * 45, ck_lo, ck_hi) == exp_ck
+        assert c.stats()["merge"] == _lib.HM_MERGE_RCCL
+        assert c.scan(b"bradfitz", 5, 4) == (MAX, 0)  # empty range through the merge
         c.set_option(_lib.HM_OPT_GRID_PER_CU, 1)
         assert c.scan(b"jonny greenwood", lo, hi) == exp
+        c.set_option(_lib.HM_OPT_MERGE_RCCL, 0)
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        assert c.stats()["merge"] == _lib.HM_MERGE_NONE
     with _lib.Context() as c:  # every visible device
         assert c.scan(b"jonny greenwood", lo, hi) == exp
+    with _lib.Context([0, 0]) as c:  # one RCCL rank per device: duplicates are refused
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        assert c.stats()["merge"] == _lib.HM_MERGE_HOST
+        c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+        with pytest.raises(_lib.HipMinerError) as ei:
+            c.scan(b"jonny greenwood", lo, hi)
+        assert ei.value.rc == _lib.HM_ERR_INVALID
 
 
 def test_miner_eval_request_on_gpu(ctx, golden):
@@ -168,7 +199,22 @@ def test_stats_accounting(ctx):
     assert st["dom_kernel"] == "hm_tiled_kernel<4, false, false>"
     assert st["dom_nonces"] == 900_000_000 + 2**32 - 10**9 and st["dom_launches"] == 2
     assert st["dom_compressions"] == 1 and st["dom_kind"] == _lib.HM_KIND_TILED
+    assert st["dom_compressions_eff"] == 1.0
     assert 0 < st["dom_kernel_ms"] <= st["kernel_ms"] <= st["wall_ms"] * 1.5
+    # config 3: two tail blocks (C = 2), the chained kernel hoists block 0 out
+    # of its loop: 1 + 1/tch compressions per nonce (tch = 1000 for f = 3)
+    rng = random.Random(440)
+    long120 = bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
+    ctx.scan(long120, 10**9, 10**9 + 10**8)
+    st = ctx.stats()
+    assert st["dom_kind"] == _lib.HM_KIND_CHAINED and st["dom_compressions"] == 2
+    assert st["dom_compressions_eff"] == pytest.approx(1.001)
+    # a scan_many batch over several chunks times every launch against one
+    # origin: the union of launch intervals is positive and below the wall time
+    ctx.scan_many([(b"bradfitz", 10**9 + 10**7 * i, 10**9 + 10**7 * (i + 1) - 1)
+                   for i in range(130)])
+    st = ctx.stats()
+    assert st["launches"] >= 130 and 0 < st["kernel_ms"] <= st["wall_ms"] * 1.5
 
 
 def test_server_model_end_to_end_gpu(ctx, oracle_mod):
