@@ -172,7 +172,24 @@ def rw(text):
     return regs(parts[0]), regs(",".join(parts[1:]))
 
 
-def plan_fixes(insts, lo, hi, text):
+# instructions whose inputs are subject to gfx950 wait-state rules (lane
+# crossing, VGPR -> SGPR reads) or that are such padding themselves: a swap
+# must not bring a VALU write closer to them
+HAZARD = re.compile(r"readlane|readfirstlane|writelane|permlane|_dpp|row_|quad_perm|"
+                    r"bank_mask|s_nop|s_setreg|s_getreg|v_cmpx")
+
+
+def same_block(between):
+    """True when the source lines between two instructions hold no label or
+    directive (only blank lines and comments), i.e. both sit in one block."""
+    for line in between:
+        t = line.strip()
+        if t and not t.startswith(";") and not t.startswith("//"):
+            return False
+    return True
+
+
+def plan_fixes(insts, lo, hi, text, between=None):
     """Make every 8-byte VALU instruction of insts[lo..hi] start at 4 mod 8.
 
     Returns (order, promote, nops): the new order of the loop's instruction
@@ -181,7 +198,10 @@ def plan_fixes(insts, lo, hi, text):
     instructions an odd number of 4-byte instructions flips the parity; each
     such gap gets one fix, cheapest first: re-encode a full-rate 4-byte VALU
     op of the gap as e64; move the gap's last 4-byte VALU op behind the next
-    8-byte instruction when the two are independent; else insert s_nop."""
+    8-byte instruction when the two are independent, in one basic block
+    (`between[p]` = the source lines separating loop slots p-1 and p) and
+    no hazard-sensitive instruction follows within three slots; else insert
+    s_nop."""
     order = list(range(lo, hi + 1))
     promote, nops = set(), set()
     if ALL_E64:
@@ -210,7 +230,10 @@ def plan_fixes(insts, lo, hi, text):
                     promote.add(order[prom[-1]])
                     addr += 4
                 elif (last == pos - 1 and insts[order[last]][2] in MOVABLE
-                      and PLAIN8.match(op)):
+                      and PLAIN8.match(op)
+                      and (between is None or same_block(between[pos]))
+                      and not any(HAZARD.search(text[order[q]])
+                                  for q in range(pos + 1, min(pos + 4, len(order))))):
                     lw, lr = rw(text[order[last]])
                     ew, er = rw(text[k])
                     if not (lw & (ew | er)) and not (ew & lr):
@@ -234,6 +257,53 @@ def plan_fixes(insts, lo, hi, text):
         addr += size
         pos += 1
     return order, promote, nops
+
+
+def blocks(lines, drop_nops):
+    """Per basic block (split at labels): the non-VALU instructions with their
+    index among the block's instructions, and the sorted VALU instructions,
+    normalised (e64 re-encodings undone; with drop_nops, `s_nop 0` lines --
+    the ones the pass inserts -- left out)."""
+    undo = {v: k for k, v in PROMOTE.items()}
+    out, cur = [], None
+    for line in lines:
+        t = line.split(";")[0].split("//")[0].strip()
+        if not t:
+            continue
+        if re.match(r"^[\w.$]+:", t):
+            cur = [t, [], []]
+            out.append(cur)
+            continue
+        m = INST.match(line)
+        if not m or cur is None:
+            continue
+        if drop_nops and t == "s_nop 0":
+            continue
+        op = m.group(1)
+        t = t.replace(op, undo.get(op, op), 1)
+        n = len(cur[1]) + len(cur[2])
+        if op.startswith("v_"):
+            cur[2].append(t)
+        else:
+            cur[1].append((n, t))
+    return [(lab, scal, sorted(vec)) for lab, scal, vec in out]
+
+
+def check_blocks(before, after):
+    """The pass only re-encodes, swaps VALU ops inside a block and adds
+    `s_nop 0`: every block must keep its label, its scalar/control
+    instructions at the same positions and the same multiset of VALU ops
+    (`s_nop 0` ignored on both sides; the count of the compiler's own is
+    checked separately: the pass never removes one)."""
+    a, b = blocks(before, True), blocks(after, True)
+    if len(a) != len(b):
+        raise SystemExit(f"block structure changed: {len(a)} -> {len(b)} blocks")
+    nops = lambda ls: sum(1 for l in ls if l.split(";")[0].strip() == "s_nop 0")
+    if nops(after) < nops(before):
+        raise SystemExit("the placement pass lost an s_nop")
+    for x, y in zip(a, b):
+        if x != y:
+            raise SystemExit(f"block {x[0]} changed by the placement pass")
 
 
 def main():
@@ -270,7 +340,8 @@ def main():
                                      f"'{lines[idx[k]].strip()}' in the source")
             lo, hi = loop
             text = {k: lines[idx[k]] for k in range(lo, hi + 1)}
-            order, promote, nops = plan_fixes(insts, lo, hi, text)
+            between = {p: lines[idx[lo + p - 1] + 1: idx[lo + p]] for p in range(1, hi - lo + 1)}
+            order, promote, nops = plan_fixes(insts, lo, hi, text, between)
             new = {}
             for k in range(lo, hi + 1):
                 t = text[k]
@@ -292,6 +363,7 @@ def main():
         assemble(dst, obj2)
         with open(dst) as f:
             lines2 = f.read().split("\n")
+        check_blocks(lines, lines2)
         where2 = source_insts(lines2)
         for sym, insts in disassemble(obj2).items():
             if sym not in loops:

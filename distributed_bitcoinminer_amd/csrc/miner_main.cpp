@@ -2,10 +2,11 @@
 // reference server.  Usage:  hm_miner <host:port>
 //
 // It does what cmu440/bitcoin/miner/miner.go does -- join with a Join message
-// (:41-51), then for every Request reply with NewResult(hash, nonce)
-// (:53-85) -- but over the native LSP client (lsp_client.cpp) and with the
-// scan (:63-76) on the GPU through hm_scan.  The `upper := Upper+1` uint64
-// wrap (:69) is kept.  A GPU failure ends the process (no CPU fallback), like
+// (joinWithServer, :24-34), then for every Request reply with
+// NewResult(hash, nonce) (evalRoutine, :36-68; Result write :60-62) -- but
+// over the native LSP client (lsp_client.cpp) and with the scan (:46-59,
+// init :48-49) on the GPU through hm_scan.  The `upper := Upper+1` uint64
+// wrap (:52) is kept.  A GPU failure ends the process (no CPU fallback), like
 // an LSP error ends the reference miner; the server then reassigns the chunk
 // (server.go:326-376).
 //

@@ -19,15 +19,15 @@
  *     built with go1.10.3); it is restated here from FIPS 180-4.
  *
  *   oracle_scan   <- cmu440/bitcoin/miner/miner.go:46-59
- *       result = maxUint; index = 0                               (:65-66)
- *       for i := lower; i < upper; i++ { if hash < result {...} } (:70-76)
+ *       result = maxUint; index = 0                               (:48-49)
+ *       for i := lower; i < upper; i++ { if hash < result {...} } (:53-59)
  *     over the truly inclusive range [lo, hi] (hi may be 2^64-1).  Ties keep
  *     the lowest nonce (strict <, ascending).  Multi-threaded runs split the
  *     range into contiguous chunks and merge lexicographically on
  *     (hash, nonce), which is equivalent to one ascending strict-< scan.
  *
  *   oracle_miner_eval <- miner.go:50-59 including the `upper := Upper+1`
- *     wrap (:69): Upper == 2^64-1 scans nothing and returns (MaxUint64, 0).
+ *     wrap (:52): Upper == 2^64-1 scans nothing and returns (MaxUint64, 0).
  *
  * Parity status: the reference ships no golden vectors for this path and its
  * Go toolchain is absent, so this restatement is pinned to FIPS 180-4 KATs

@@ -71,6 +71,46 @@ def test_moves_respect_dependencies(monkeypatch):
     assert order == [0, 2, 1] and not nops and not promote
 
 
+def test_moves_stay_in_their_block_and_clear_of_hazards(monkeypatch):
+    """No swap across a label (another basic block) or in front of an
+    instruction with wait-state rules (DPP / permlane / readlane): s_nop."""
+    monkeypatch.setattr(al, "ALL_E64", False)
+    spec = [(8, "v_alignbit_b32"), (4, "v_lshlrev_b32_e32"), (8, "v_bitop3_b32"),
+            (8, "v_add3_u32")]
+    insts = _insts(spec, base=0x104)
+    text = {0: "\tv_alignbit_b32 v1, v2, v2, 7", 1: "\tv_lshlrev_b32_e32 v7, 2, v1",
+            2: "\tv_bitop3_b32 v4, v3, v5, v6 bitop3:0x96", 3: "\tv_add3_u32 v8, v9, v9, v9"}
+    between = {1: [], 2: [".LBB0_7:"], 3: []}
+    order, promote, nops = al.plan_fixes(insts, 0, 3, text, between)
+    assert order == [0, 1, 2, 3] and nops == {2}
+    between[2] = ["\t; comment only"]
+    order, promote, nops = al.plan_fixes(insts, 0, 3, text, between)
+    assert order == [0, 2, 3, 1] and not nops  # moved behind both (independent)
+    text[3] = "\tv_permlane32_swap_b32_e32 v7, v9"
+    order, promote, nops = al.plan_fixes(insts, 0, 3, text, between)
+    assert order == [0, 1, 2, 3] and nops == {2}
+
+
+def test_block_structure_check():
+    before = ["k:", "\tv_add_u32_e32 v1, v2, v3", "\ts_add_i32 s0, s1, 1",
+              "\tv_xor_b32_e32 v4, v5, v6", ".LBB0_1:", "\tv_alignbit_b32 v1, v1, v1, 2",
+              "\ts_cbranch_scc1 .LBB0_1"]
+    ok = ["k:", "\tv_add_u32_e64 v1, v2, v3", "\ts_add_i32 s0, s1, 1",
+          "\ts_nop 0", "\tv_xor_b32_e32 v4, v5, v6", ".LBB0_1:",
+          "\tv_alignbit_b32 v1, v1, v1, 2", "\ts_cbranch_scc1 .LBB0_1"]
+    al.check_blocks(before, ok)
+    moved = ["k:", "\tv_add_u32_e32 v1, v2, v3", "\ts_add_i32 s0, s1, 1", ".LBB0_1:",
+             "\tv_xor_b32_e32 v4, v5, v6", "\tv_alignbit_b32 v1, v1, v1, 2",
+             "\ts_cbranch_scc1 .LBB0_1"]
+    with pytest.raises(SystemExit):
+        al.check_blocks(before, moved)
+    scalar_moved = ["k:", "\ts_add_i32 s0, s1, 1", "\tv_add_u32_e32 v1, v2, v3",
+                    "\tv_xor_b32_e32 v4, v5, v6", ".LBB0_1:", "\tv_alignbit_b32 v1, v1, v1, 2",
+                    "\ts_cbranch_scc1 .LBB0_1"]
+    with pytest.raises(SystemExit):
+        al.check_blocks(before, scalar_moved)
+
+
 @pytest.mark.skipif(not os.path.exists(ALIGNED), reason="library not built")
 def test_shipped_scan_kernels_are_placed():
     with open(ALIGNED) as f:

@@ -7,6 +7,9 @@ SQ_INSTS_VALU per 64-nonce wave-iteration, effective clock
 (GRBM_GUI_ACTIVE / 8 / duration, MI355X_MICROARCH.md 'DVFS give-back'),
 and HBM bytes per launch: FETCH_SIZE x 2 (gfx950 reports half of wide reads,
 MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KB.
+Each entry records the sha256 (16 hex) of the scan code object it was measured
+on (build/hipminer/hipminer_scan.hsaco); bench.py uses an entry only for that
+same build.
 usage: python tools/summarize_profile.py gpurun_out/r01 profiles/r01
 """
 import collections
@@ -34,6 +37,10 @@ def per_dispatch(path):
     return d
 
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import code_object_sha16  # noqa: E402
+
+SHA = code_object_sha16()
 out = {}
 valu = per_dispatch(os.path.join(src, "pmc_valu", "run_counter_collection.csv"))
 fetch = per_dispatch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"))
@@ -59,6 +66,7 @@ for name, nonces in NONCES.items():
         "cycles_per_wave_inst": (dur * 1e-9 * grbm / 8 / dur * 1e9) / (insts / 1024) if insts else None,
         "fetch_kb_raw": fetch_kb, "write_kb": write_kb,
         "hbm_bytes_per_launch": (2 * fetch_kb + write_kb) * 1024 / n_l,
+        "code_object_sha16": SHA,
     }
 os.makedirs(dst, exist_ok=True)
 if os.path.exists(merge_into):  # keep kernels summarised from other runs
