@@ -95,3 +95,17 @@ def test_config5_chunks_checked(ctx):
                 assert _triple(ch) == ((MAX, 0), 0, 0)
                 continue
             assert ctx.scan_checked(m, a, b) == _triple(ch), (case["name"], a, b)
+
+
+def test_medium_random_fixtures(ctx):
+    """153 random ranges of 10^6..2*10^8 nonces (every message length 0..130,
+    digit-count changes, next to 2^64-1; tests/golden/gen_medium.py) through
+    hm_scan_checked and hm_scan against the oracle's triples."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "medium.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) >= 150
+    for c in cases:
+        m, lo, hi = bytes.fromhex(c["msg_hex"]), int(c["lo"]), int(c["hi"])
+        exp = _triple(c)
+        assert ctx.scan_checked(m, lo, hi) == exp, c["name"]
+        assert ctx.scan(m, lo, hi) == exp[0], c["name"]

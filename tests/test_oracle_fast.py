@@ -49,3 +49,17 @@ def test_fast_matches_large_fixture_slice():
     """A 2^24 slice of config 2's fixture range, both oracles."""
     lo, hi = 4_000_000_000, 4_000_000_000 + (1 << 24)
     assert O.fast_scan_sum(b"bradfitz", lo, hi) == O.c_scan_sum(b"bradfitz", lo, hi, threads=8)
+
+
+def test_medium_fixtures_agree_with_plain_oracle():
+    """The smallest cases of tests/golden/medium.json (written by the fast
+    oracle) recomputed by the plain oracle."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "medium.json")) as f:
+        cases = json.load(f)["cases"]
+    small = sorted(cases, key=lambda c: int(c["count"]) * (1 + len(c["msg_hex"]) // 110))[:8]
+    for c in small:
+        m, lo, hi = bytes.fromhex(c["msg_hex"]), int(c["lo"]), int(c["hi"])
+        exp = ((int(c["hash"]), int(c["nonce"])), int(c["sum"]), int(c["count"]))
+        assert O.c_scan_sum(m, lo, hi, threads=8) == exp, c["name"]
