@@ -59,6 +59,39 @@ WORKLOADS = {
 }
 
 
+def fixture_check(msg: bytes, lo: int, hi: int, res):
+    """Compare a whole-job answer with the committed oracle fixture of the
+    same (message, range), if there is one: tests/golden/large.json (configs
+    [1]/[2] over [0, 2^32)) and full_size.json (configs[3] over [0, 2^40),
+    and the weak-scaling jobs [0, N*2^32) of configs[1]/[2] for N <= 8).
+    Data only -- nothing under oracle/ is run here."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    found = []
+    try:
+        with open(os.path.join(gold, "large.json")) as f:
+            for c in json.load(f):
+                found.append(("tests/golden/large.json", c))
+        with open(os.path.join(gold, "full_size.json")) as f:
+            full = json.load(f)
+        c4 = full.get("cfg4")
+        if c4:
+            found.append(("tests/golden/full_size.json", dict(c4, **c4["whole"])))
+        for w in full.get("weak", []):  # [0, N*2^32): the first N pieces
+            for n in range(1, len(w["pieces"]) + 1):
+                best = min((int(p["hash"]), int(p["nonce"])) for p in w["pieces"][:n])
+                found.append(("tests/golden/full_size.json",
+                              {"msg_hex": w["msg_hex"], "lo": "0", "hi": str((n << 32) - 1),
+                               "hash": str(best[0]), "nonce": str(best[1])}))
+    except (OSError, ValueError):
+        return None
+    for path, c in found:
+        if bytes.fromhex(c["msg_hex"]) == msg and (int(c["lo"]), int(c["hi"])) == (lo, hi):
+            exp = (int(c["hash"]), int(c["nonce"]))
+            return {"fixture": path, "expected": {"hash": exp[0], "nonce": exp[1]},
+                    "match": tuple(res) == exp}
+    return None
+
+
 def code_object_sha16():
     """sha256 (16 hex) of the scan kernels' code object this tree built
     (build/hipminer/hipminer_scan.hsaco, embedded in libhipminer.so)."""
@@ -310,6 +343,7 @@ def main():
                 "ms_per_step": round(e3 / steps3 * 1e3, 3),
                 "ms_per_step_median_rank0": round(sorted(sm3)[len(sm3) // 2], 3),
                 "result": {"hash": r3[0], "nonce": r3[1]},
+                "result_vs_oracle": fixture_check(m3, 0, total_nonces - 1, r3),
                 "roofline": roofline(st3, m3, lo, hi)}}
 
     if rank == 0:
@@ -334,6 +368,7 @@ def main():
                        "merge": ("RCCL all-gather" if backend == "nccl" else backend)
                                 if dist is not None else "none (1 rank)"},
             "result": {"hash": res[0], "nonce": res[1]},
+            "result_vs_oracle": fixture_check(msg, 0, total_nonces - 1, res),
             "roofline": rl,
         }
         if secondary:

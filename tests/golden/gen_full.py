@@ -8,6 +8,10 @@ midstate; checked against oracle/hm_oracle.c by tests/test_oracle_fast.py).
   each piece records (min hash, nonce, sum of keys mod 2^64, count).  Any
   shard made of whole pieces -- in particular every rank's shard of a 1..8-GPU
   run -- is pinned by merging its pieces.  About 3 h on 8 cores.
+* weak: bench.py's weak-scaling ranges: rank r of N scans [r*2^32,
+  (r+1)*2^32) of configs[1]'s "bradfitz" and configs[2]'s 120-B message, so
+  the whole job of an N-GPU run is [0, N*2^32); one piece per 2^32 for
+  r = 0..7 pins N = 1..8.  About 20 min.
 * cfg5: the four SURVEY messages, each as a client Request
   [2^64-1-2^34, 2^64-2] split by the reference server into 8 miner chunks
   (server.go:165-205, restated in server_model.load_balance); every chunk's
@@ -108,6 +112,16 @@ def main():
                      "upper": str(CFG5_UP), "miners": CFG5_MINERS, "chunks": res,
                      "client_result": {"hash": str(merged[0]), "nonce": str(merged[1])}})
     out["cfg5"] = cfg5
+    if not args.cfg5_only:
+        weak = []
+        for name, msg in (("bradfitz", CFG4_MSG), ("long120", long120())):
+            pcs = []
+            for r in range(8):
+                p = dict(piece(f"weak:{name}:{r}", msg, r << 32, ((r + 1) << 32) - 1))
+                p.pop("key")
+                pcs.append(p)
+            weak.append({"name": name, "msg_hex": msg.hex(), "pieces": pcs})
+        out["weak"] = weak
     if args.cfg5_only:
         if os.path.exists(OUT):
             with open(OUT) as f:

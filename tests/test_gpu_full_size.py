@@ -109,3 +109,23 @@ def test_medium_random_fixtures(ctx):
         exp = _triple(c)
         assert ctx.scan_checked(m, lo, hi) == exp, c["name"]
         assert ctx.scan(m, lo, hi) == exp[0], c["name"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", ["bradfitz", "long120"])
+def test_weak_scaling_rank_shards(ctx, name):
+    """bench.py's weak-scaling work at N = 8 (configs[1] / configs[2]): rank
+    r scans [r*2^32, (r+1)*2^32).  Every rank's shard through hm_scan_checked
+    equals the oracle's piece, so each rank's answer of the driver's 8-GPU run
+    and their merge (what the all-gather produces) are pinned."""
+    fx = _fixture()
+    w = next(x for x in fx["weak"] if x["name"] == name)
+    m = bytes.fromhex(w["msg_hex"])
+    got = []
+    for r, p in enumerate(w["pieces"]):
+        lo, hi = r << 32, ((r + 1) << 32) - 1
+        assert (int(p["lo"]), int(p["hi"])) == (lo, hi)
+        t = ctx.scan_checked(m, lo, hi)
+        assert t == _triple(p), (name, r)
+        got.append(t)
+    assert _merge(got)[2] == 8 << 32
