@@ -227,6 +227,11 @@ def roofline(st, msg, lo, hi):
 
 
 def main():
+    # stdout carries exactly one JSON line (rank 0): whatever the libraries
+    # print (RCCL's version banner, gloo's connection notes) goes to stderr
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -376,7 +381,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(msg, args.workload)
             line["cpu_baseline"] = cb
-        print(json.dumps(line), flush=True)
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
