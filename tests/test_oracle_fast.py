@@ -63,3 +63,23 @@ def test_medium_fixtures_agree_with_plain_oracle():
         m, lo, hi = bytes.fromhex(c["msg_hex"]), int(c["lo"]), int(c["hi"])
         exp = ((int(c["hash"]), int(c["nonce"])), int(c["sum"]), int(c["count"]))
         assert O.c_scan_sum(m, lo, hi, threads=8) == exp, c["name"]
+
+
+def test_full_size_fixtures_agree_at_2p32():
+    """Both oracles at the full 2^32 of configs[1] and configs[2]: the first
+    weak-scaling piece of tests/golden/full_size.json (fast oracle) equals
+    tests/golden/large.json (plain oracle, 8 threads) -- min, sum of all
+    2^32 keys and count."""
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(__file__), "golden")
+    with open(os.path.join(gold, "large.json")) as f:
+        large = {c["msg_hex"]: c for c in json.load(f)}
+    with open(os.path.join(gold, "full_size.json")) as f:
+        weak = json.load(f)["weak"]
+    assert len(weak) == 2
+    for w in weak:
+        p, c = w["pieces"][0], large[w["msg_hex"]]
+        assert (p["lo"], p["hi"]) == (c["lo"], c["hi"]) == ("0", str(2**32 - 1))
+        for k in ("hash", "nonce", "sum", "count"):
+            assert p[k] == c[k], (w["name"], k)
