@@ -233,12 +233,12 @@ def partition(msg, lo: int, hi: int, n: int) -> list:
 def debug_plan(msg, lo: int, hi: int, force_generic: bool = False) -> list[dict]:
     m = as_bytes(msg)
     cap = 32
-    buf = (ctypes.c_int64 * (9 * cap))()
+    buf = (ctypes.c_int64 * (10 * cap))()
     n = load().hm_debug_plan(m, len(m), lo, hi, int(force_generic), buf, cap)
-    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost")
+    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost", "lane3")
     out = []
     for i in range(min(n, cap)):
-        row = dict(zip(keys, buf[9 * i: 9 * i + 9]))
+        row = dict(zip(keys, buf[10 * i: 10 * i + 10]))
         row["lo"] &= (1 << 64) - 1
         row["hi"] &= (1 << 64) - 1
         out.append(row)

@@ -946,7 +946,7 @@ int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
 
 // ---- debug exports for host-side tests (not part of include/hipminer.h) ----
 // Writes up to `cap` segment descriptors as 9 x int64:
-//   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces)
+//   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces), lane3
 int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
                   int64_t* outv, int cap) {
     if (lo > hi) return 0;
@@ -961,10 +961,11 @@ int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int 
     int i = 0;
     for (; i < (int)segs.size() && i < cap; ++i) {
         const SegPlan& s = segs[i];
-        int64_t* o = outv + 9 * i;
+        int64_t* o = outv + 10 * i;
         o[0] = s.d; o[1] = (int64_t)s.lo; o[2] = (int64_t)s.hi; o[3] = s.kind;
         o[4] = s.W1; o[5] = s.V; o[6] = s.trailer; o[7] = s.straddle;
         o[8] = (int64_t)seg_cost(s);
+        o[9] = s.lane3;
     }
     return (int)segs.size();
 }

@@ -31,6 +31,7 @@ struct SegPlan {
     // tiled layout
     int W1;                     // word holding the last digit (varying words W1-1, W1)
     bool straddle, trailer;
+    bool lane3;                 // lane digits reach back into W[W1-2] (q = 5 where two words give 3-4)
     uint32_t V, q;              // varying digits; lane digits (V = q + 2 loop digits)
     uint32_t lane_shift, loop_shift;
     uint64_t pow10V;

@@ -47,6 +47,12 @@ namespace hm {
 template <int W1, bool STRADDLE, bool TRAILER, bool CSUM>
 DEV void tiled_body(const TiledArgs& A) {
     static_assert(W1 >= 1 && W1 <= 15, "varying words are W[W1-1], W[W1]");
+    // Lane digits may reach back into W[W1-2] (the planner does so when the
+    // last two words leave room for fewer than 5 lane digits: 10^3 or 10^4
+    // lane values fill 64-lane chunks only to 97.7 / 99.5 %).  W[W1-2] is
+    // loop-invariant, so this changes per-task work only: the hot loop's
+    // instructions are the same (profiles/r02/isa_audit.txt).
+    constexpr bool L3 = W1 >= 2;
     const uint32_t lane = __lane_id();
     const uint32_t wslot = blockIdx.x * (kBlock / kWaveSize) + uni(threadIdx.x / kWaveSize);
     uint32_t best_hi = 0xffffffffu, best_lo = 0xffffffffu;  // wave-uniform (SGPR)
@@ -86,9 +92,18 @@ DEV void tiled_body(const TiledArgs& A) {
             packed |= (uint64_t)(0x30u + x - y * 10u) << (8u * k);
             x = y;
         }
-        packed <<= A.lane_shift;
-        const uint32_t X0 = W[W1 - 1] | (uint32_t)(packed >> 32);
-        const uint32_t X1 = W[W1] | (uint32_t)packed;
+        // the lane digits as a 96-bit big-endian window W[W1-2]:W[W1-1]:W[W1]
+        uint32_t Xm2 = 0, X0, X1;
+        if constexpr (L3) {
+            const unsigned __int128 p = (unsigned __int128)packed << A.lane_shift;
+            Xm2 = W[W1 - 2] | (uint32_t)(p >> 64);
+            X0 = W[W1 - 1] | (uint32_t)(p >> 32);
+            X1 = W[W1] | (uint32_t)p;
+        } else {
+            packed <<= A.lane_shift;  // fits: q + lane_shift/8 <= 8 bytes
+            X0 = W[W1 - 1] | (uint32_t)(packed >> 32);
+            X1 = W[W1] | (uint32_t)packed;
+        }
         const uint64_t nbase = (A.tile0 + tile) * A.pow10V + (uint64_t)v * 100u;
         const uint32_t s0X1 = ssig0<false>(X1);  // lane part of sigma0(W[W1])
 
@@ -97,6 +112,7 @@ DEV void tiled_body(const TiledArgs& A) {
                 uint32_t m[16];
 #pragma unroll
                 for (int k = 0; k < 16; ++k) m[k] = W[k];
+                if constexpr (L3) m[W1 - 2] = Xm2;
                 // loop digits: wave-uniform, in bytes that are zero in X1
                 uint32_t L;
                 if constexpr (STRADDLE) {

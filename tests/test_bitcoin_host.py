@@ -105,8 +105,15 @@ def test_planner_layouts(L):
             first = p_end - V + 1                    # first varying byte in block fb
             digit_start = r if fb == 0 else 0
             assert 5 <= V <= 8 and V <= d
-            assert first >= digit_start and first >= 4 * (s["W1"] - 1)
             assert s["W1"] >= 1
+            if s["lane3"]:  # lanes reach into W[W1-2]: only where two words give q < 5
+                assert s["W1"] >= 2 and p_end % 4 in (0, 1) and V <= 7
+                assert first >= digit_start and first >= 4 * (s["W1"] - 2)
+                assert first < 4 * (s["W1"] - 1)
+            else:
+                assert first >= digit_start and first >= 4 * (s["W1"] - 1)
+                # two words were enough, or the message prefix leaves no room
+                assert V >= 7 or s["W1"] < 2 or first == digit_start
             assert (not s["trailer"]) or s["W1"] >= 13
         elif s["kind"] == _lib.HM_KIND_CHAINED:
             f = T - 64                              # digits in the final block

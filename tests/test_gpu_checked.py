@@ -88,7 +88,7 @@ def test_checked_whole_tiles_vs_generic(ctx):
             seg = _lib.debug_plan(m, dlo, dhi)[0]
             if seg["kind"] == _lib.HM_KIND_GENERIC:
                 continue
-            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"])
+            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"], seg["lane3"])
             if key in seen:
                 continue
             seen.add(key)
@@ -156,19 +156,21 @@ def test_checked_full_size_pinned(ctx, case):
 
 
 def test_checked_beyond_cpu(ctx):
-    """1.2e11 nonces of bradfitz at d=12 (two chunked launches of 2^20 tiles):
-    no CPU can rescan it, so the count must be exact, shards split at the launch
-    boundary and elsewhere must add up, and a window around the boundary must
-    match the generic kernel."""
+    """1.2e11 nonces at d=12 as two chunked launches of 2^20 tiles (a 56-B
+    message: two-block tail, W1 = 1, 10^5-nonce tiles), and 1.2e11 nonces of
+    bradfitz at d=12 (three-word lanes, one launch): no CPU can rescan them,
+    so the counts must be exact, shards split at the launch boundary and
+    elsewhere must add up, and windows must match the generic kernel."""
     lo, hi = 10**11, 10**11 + 120_000_000_000
-    whole = ctx.scan_checked(b"bradfitz", lo, hi)
-    assert whole[2] == hi - lo + 1
-    boundary = (lo // 10**5 + (1 << 20)) * 10**5
-    cuts = [lo, lo + 7_777_777_777, boundary - 3, boundary + 5, hi + 1]
-    assert _add([ctx.scan_checked(b"bradfitz", a, b - 1) for a, b in zip(cuts, cuts[1:])]) == whole
-    w_lo, w_hi = boundary - 20_000_000, boundary + 20_000_000
-    assert ctx.scan_checked(b"bradfitz", w_lo, w_hi) == _generic(ctx, b"bradfitz", w_lo, w_hi)
-    assert _lib.host_hash(b"bradfitz", whole[0][1]) == whole[0][0]
+    for m in (b"x" * 56, b"bradfitz"):
+        whole = ctx.scan_checked(m, lo, hi)
+        assert whole[2] == hi - lo + 1
+        boundary = (lo // 10**5 + (1 << 20)) * 10**5
+        cuts = [lo, lo + 7_777_777_777, boundary - 3, boundary + 5, hi + 1]
+        assert _add([ctx.scan_checked(m, a, b - 1) for a, b in zip(cuts, cuts[1:])]) == whole
+        w_lo, w_hi = boundary - 20_000_000, boundary + 20_000_000
+        assert ctx.scan_checked(m, w_lo, w_hi) == _generic(ctx, m, w_lo, w_hi)
+        assert _lib.host_hash(m, whole[0][1]) == whole[0][0]
 
 
 def test_checked_multi_device_and_streams(oracle_mod):

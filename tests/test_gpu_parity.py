@@ -257,7 +257,7 @@ def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
             seg = _lib.debug_plan(m, dlo, dhi)[0]
             if seg["kind"] == _lib.HM_KIND_GENERIC:
                 continue
-            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"])
+            key = (seg["kind"], seg["W1"], seg["straddle"], seg["trailer"], seg["V"], seg["lane3"])
             if key in seen:
                 continue
             seen.add(key)
@@ -314,24 +314,26 @@ def test_scan_many_batches(oracle_mod):
 
 
 def test_chunked_tile_launches(ctx):
-    """A segment with > 2^20 tiles is split into several launches (config 4 at
-    d=13 does this).  bradfitz at d=12 has V=5 (10^5-nonce tiles): 1.2e11
-    nonces = 1.2 M tiles -> 2 launches.  Checked by shard invariance across the
-    launch boundary and the generic kernel on a window around it."""
+    """A segment with > 2^20 tiles is split into several launches.  A 56-B
+    message at d=12 has a two-block tail whose last digit opens word 1 of
+    block 1 (W1 = 1, no room for three-word lanes): V=5, 10^5-nonce tiles, so
+    1.2e11 nonces = 1.2 M tiles -> 2 launches.  Checked by shard invariance
+    across the launch boundary and the generic kernel on a window around it."""
     from distributed_bitcoinminer_amd.parallel import merge
+    m = b"x" * 56
     lo, hi = 10**11, 10**11 + 120_000_000_000
-    seg = _lib.debug_plan(b"bradfitz", lo, hi)[0]
-    assert seg["kind"] == _lib.HM_KIND_TILED and seg["V"] == 5
-    whole = ctx.scan(b"bradfitz", lo, hi)
+    seg = _lib.debug_plan(m, lo, hi)[0]
+    assert seg["kind"] == _lib.HM_KIND_TILED and seg["V"] == 5 and seg["W1"] == 1
+    whole = ctx.scan(m, lo, hi)
     assert ctx.stats()["dom_launches"] >= 2
     boundary = (lo // 10**5 + (1 << 20)) * 10**5  # first nonce of the 2nd launch
-    parts = [ctx.scan(b"bradfitz", lo, boundary - 7), ctx.scan(b"bradfitz", boundary - 6, hi)]
+    parts = [ctx.scan(m, lo, boundary - 7), ctx.scan(m, boundary - 6, hi)]
     assert merge(parts) == whole
     w_lo, w_hi = boundary - 30_000_000, boundary + 30_000_000
-    fast = ctx.scan(b"bradfitz", w_lo, w_hi)
+    fast = ctx.scan(m, w_lo, w_hi)
     ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
     try:
-        assert ctx.scan(b"bradfitz", w_lo, w_hi) == fast
+        assert ctx.scan(m, w_lo, w_hi) == fast
     finally:
         ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
-    assert _lib.host_hash(b"bradfitz", whole[1]) == whole[0]
+    assert _lib.host_hash(m, whole[1]) == whole[0]
