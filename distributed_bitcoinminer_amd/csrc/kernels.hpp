@@ -65,7 +65,7 @@ struct TiledArgs {
 };
 
 // Chained scan (two-block tails whose final block holds only 1..4 digits):
-// lanes vary the last q digits of tail block 0 (word W15), the final
+// lanes vary the last q <= 5 digits of tail block 0 (W15, W14's last byte), the final
 // block's digits are the loop index t and its schedule comes from a table of
 // K[i]+W[i] (kMaxChainedTable entries x 64 words).
 constexpr uint32_t kMaxChainedF = 4;
@@ -86,7 +86,7 @@ struct ChainedArgs {
     uint32_t ntc;            // loop chunks per lane chunk
     uint32_t tch;            // loop values per loop chunk
     uint32_t vmax;           // 10^q - 1
-    uint32_t q;              // lane digits (<= 4, all in W15)
+    uint32_t q;              // lane digits (<= 5: W15 and the last byte of W14)
 };
 
 // Generic scan: one nonce per lane (small / irregular segments, cross-checks).

@@ -228,18 +228,22 @@ DEV void chained_body(const ChainedArgs& A) {
         uint32_t v = chunk * kWaveSize + lane;
         const bool lane_ok = v <= A.vmax;
         v = v > A.vmax ? A.vmax : v;
-        uint32_t packed = 0, x = v;
+        // lane digits: the last q (<= 5) bytes of tail block 0, in W15 and
+        // (q = 5) the last byte of W14
+        uint64_t packed = 0;
+        uint32_t x = v;
         for (uint32_t k = 0; k < A.q; ++k) {
             const uint32_t y = x / 10u;
-            packed |= (0x30u + x - y * 10u) << (8u * k);
+            packed |= (uint64_t)(0x30u + x - y * 10u) << (8u * k);
             x = y;
         }
         uint32_t m[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) m[k] = W[k];
-        m[15] = W[15] | packed;
+        m[14] = W[14] | (uint32_t)(packed >> 32);
+        m[15] = W[15] | (uint32_t)packed;
         State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
-        sha_rounds<1u << 15>(s, m);
+        sha_rounds<3u << 14>(s, m);  // once per task: W14, W15 vary across lanes
         // chaining value into the final block (per lane)
         const State cs{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
                        s.e + st[4], s.f + st[5], s.g + st[6], s.h + st[7]};

@@ -118,8 +118,8 @@ def test_planner_layouts(L):
         elif s["kind"] == _lib.HM_KIND_CHAINED:
             f = T - 64                              # digits in the final block
             assert fb == 1 and 1 <= f <= 4
-            q = s["V"] - f                          # lane digits, all in W15 of block 0
-            assert 2 <= q <= 4 and q <= 64 - r
+            q = s["V"] - f                          # lane digits, W15 (+ W14's last byte) of block 0
+            assert 2 <= q <= 5 and q == min(5, 64 - r)
         else:
             assert s["kind"] == _lib.HM_KIND_GENERIC
     assert prev_hi == MAX

@@ -97,7 +97,7 @@ def test_chained_layouts_vs_oracle(ctx, oracle_mod):
             base = rng.randrange(10**(d - 1), dhi - 300_000)
             lo, hi = base, base + rng.randrange(1, 250_000)
             assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
-    assert {(1, 4), (2, 4), (3, 4), (4, 4)} <= seen
+    assert {(1, 5), (2, 5), (3, 5), (4, 5)} <= seen
 
 
 def test_long120_config3_slice(ctx, oracle_mod):

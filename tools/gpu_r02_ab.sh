@@ -8,9 +8,17 @@ O=$1; A=$2; B=$3; K=${4:-}
 mkdir -p $O
 KARG=(); [ -n "$K" ] && KARG=(-k "$K")
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread "${KARG[@]}" > $O/pytest_gpu.log 2>&1 &&
+M3=$(python -c "import random;r=random.Random(440);print(''.join(chr(r.choice(range(0x21,0x7f))) for _ in range(120)))")
+W=${AB_WORKLOADS:-tiled}
+if [ "$W" = tiled ]; then
 timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B > $O/ab_cfg2.txt 2>&1 &&
 timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- bradfitz 100000000000 120000000000 > $O/ab_d12.txt 2>&1 &&
 timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- bradfitz 1000000000000 1020000000000 > $O/ab_d13.txt 2>&1 &&
 timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- bradfitz 100000000 999999999 > $O/ab_d9.txt 2>&1
+else
+timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- "$M3" 0 4294967295 > $O/ab_cfg3.txt 2>&1 &&
+timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- "$M3" 10000000000 30000000000 > $O/ab_cfg3_d11.txt 2>&1 &&
+timeout -k 10 300 python -u tools/ab_libs.py 7 $A $B -- "$M3" 100000000 999999999 > $O/ab_cfg3_d9.txt 2>&1
+fi
 rc=$?
 tail -n 2 $O/pytest_gpu.log; cat $O/ab_*.txt; echo "ab rc=$rc"; exit $rc
