@@ -25,7 +25,9 @@ NONCES = {"hm_tiled_kernel<4, false, false>": 900_000_000 + (2**32 - 10**9),
           "hm_tiled_kernel<4, true, false>": 90_000_000,
           "hm_tiled_kernel<3, false, false>": 9_990_000,
           # cfg3 (120-B message): d = 8, 9, 10 are chained
-          "hm_chained_kernel": 2**32 - 10**7}
+          "hm_chained_kernel": 2**32 - 10**7,
+          # cfg4's dominant segment (bradfitz d = 12): [10^11, 1.2*10^11)
+          "hm_tiled_kernel<5, true, false>": 20_000_000_000}
 
 
 def per_dispatch(path):
