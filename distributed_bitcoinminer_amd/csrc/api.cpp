@@ -561,23 +561,11 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
         size_t last_dom = 0;
         for (size_t i = 0; i < segs.size(); ++i)
             if (key(segs[i]) == dom) last_dom = i;
-        // the non-dominant segments go onto the low-priority streams largest
-        // first, so the biggest of them (e.g. cfg2's d=8: 9e7 nonces) is the
-        // first kernel its stream dispatches when the gate opens and takes
-        // the slots the dominant launch's retiring waves free, instead of
-        // queueing behind a smaller segment and running after everything
-        std::vector<size_t> order(segs.size());
-        for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
-            return segs[a].hi - segs[a].lo > segs[b].hi - segs[b].lo;
-        });
         for (int pass = 0; pass < (nstreams > 1 ? 2 : 1); ++pass) {
             if (pass == 1)
                 for (int q = 1; q < nstreams; ++q)
                     HIPCHK(hipStreamWaitEvent(dv.stream[q], dv.gate, 0));
-            for (size_t j = 0; j < segs.size(); ++j) {
-                // dominant segments in ascending order on stream 0; the others by size
-                const size_t i = pass == 1 ? order[j] : j;
+            for (size_t i = 0; i < segs.size(); ++i) {
                 int si = 0;
                 if (nstreams > 1) {
                     const bool is_dom = key(segs[i]) == dom;
