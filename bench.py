@@ -106,7 +106,7 @@ def code_object_sha16():
 def profiled(kernel: str):
     """PMC summary of `kernel` from the newest committed profile
     (profiles/rNN/pmc_summary.json, written by tools/summarize_profile.py):
-    HBM bytes per launch, the effective clock and the measured VALU
+    HBM bytes per nonce, the effective clock and the measured VALU
     instructions per nonce (SQ_INSTS_VALU per 64-nonce wave iteration), with
     the file they came from.  Only a summary recorded for THIS build's code
     object (its `code_object_sha16`) counts: a stale one gives Nones."""
@@ -120,7 +120,10 @@ def profiled(kernel: str):
             k = summ[kernel]
             if sha is None or k.get("code_object_sha16") != sha:
                 return None, None, None, None
-            return k["hbm_bytes_per_launch"], k["f_eff_ghz_largest_dispatch"], \
+            # HBM bytes per nonce of the profiled workload (its launches may
+            # be sized differently from the bench's)
+            per_nonce = k["hbm_bytes_per_launch"] * k["launches"] / k["nonces"]
+            return per_nonce, k["f_eff_ghz_largest_dispatch"], \
                 k.get("valu_insts_per_wave_iteration_64_nonces"), os.path.relpath(path, ROOT)
     return None, None, None, None
 
@@ -187,7 +190,8 @@ def roofline(st, msg, lo, hi):
     nonces_pl = st["dom_nonces"] / launches
     achieved = nonces_pl * OPS_PER_COMPRESSION * C_eff / (avg_ms * 1e-3) / 1e12
     achieved_alg = nonces_pl * OPS_PER_COMPRESSION * C / (avg_ms * 1e-3) / 1e12
-    traffic, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
+    traffic_pn, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
+    traffic = round(traffic_pn * nonces_pl) if traffic_pn is not None else None
     # algorithmic HBM bytes of one dominant launch: its 128-B tile records
     # (10^V nonces each) + one 16-B candidate per wave of the grid; the
     # work queue adds one device-scope atomicAdd per dequeued task

@@ -40,8 +40,8 @@ def test_profiled_requires_this_code_object(tmp_path, monkeypatch):
     sha = bench.code_object_sha16()
     prof = tmp_path / "profiles" / "r99"
     prof.mkdir(parents=True)
-    entry = {"hbm_bytes_per_launch": 1.0, "f_eff_ghz_largest_dispatch": 2.3,
-             "valu_insts_per_wave_iteration_64_nonces": 1200.0}
+    entry = {"hbm_bytes_per_launch": 4.0, "launches": 2, "nonces": 8,
+             "f_eff_ghz_largest_dispatch": 2.3, "valu_insts_per_wave_iteration_64_nonces": 1200.0}
     (prof / "pmc_summary.json").write_text(json.dumps({"k": dict(entry, code_object_sha16="0" * 16)}))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
     monkeypatch.setattr(bench, "code_object_sha16", lambda: sha or "f" * 16)
