@@ -42,6 +42,10 @@ extern "C" const unsigned char hm_scan_code_object[];
 namespace {
 
 constexpr int kStreams = 4;
+// Requests of at most this many nonces (≈3.6 ms of work) run their digit
+// segments concurrently on all streams; larger ones use the dominant-stream
+// order with tail filling (enqueue_device_batch).
+constexpr uint64_t kConcurrentNonces = 1ull << 27;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -281,6 +285,20 @@ uint32_t guided_tasks(uint64_t nunits, int grid, uint32_t* nbig) {
     return (uint32_t)(nunits - small + kSplit * small);
 }
 
+// Grid and guided task list of a persistent launch over `nunits` units: the
+// split is planned against the occupancy-sized grid, then the grid is cut to
+// the task count (one wave per task at most).  A launch with fewer units than
+// the GPU has waves splits every unit, and sizing its grid by tasks rather
+// than units gives each task its own wave: a segment of 10^4..10^7 nonces is
+// latency-bound (one wave runs its tasks' SHA chains back to back), so this
+// cuts such launches from ≈270-390 µs to tens of µs (config 1's request).
+int plan_launch(const hm_ctx* ctx, const Device& dv, int per_cu_auto, uint64_t nunits,
+                uint32_t* ntasks, uint32_t* nbig) {
+    const int cap = persistent_grid(ctx, dv, per_cu_auto, 1ull << 40);  // occupancy-sized
+    *ntasks = guided_tasks(nunits, cap, nbig);
+    return persistent_grid(ctx, dv, per_cu_auto, *ntasks);
+}
+
 // Units of a launch over tiles [t, t+nt) (unit = lane chunk x `per_chunk`
 // loop chunks; lane value v of a tile covers nonces base + v*step + [0, step)):
 // the lane chunks of the first tile wholly below s.lo and of the last tile
@@ -353,8 +371,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         const Device::Fn* fn = nullptr;
         int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
         if (rc) return rc;
-        const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
-        ca.ntasks = guided_tasks(nunits, grid, &ca.nbig);
+        const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ca.ntasks, &ca.nbig);
         // task ids start at unit0 (the queue counter too): the kernels map a
         // task below nbig to that unit, so the skipped units are never dequeued
         ca.ntasks += unit0;
@@ -436,8 +453,8 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             const Device::Fn* fn = nullptr;
             int rc = scan_fn(dv, tiled_symbol(s, ctx->csum), &fn);
             if (rc) return rc;
-            const int grid = persistent_grid(ctx, dv, fn->blocks_per_cu, nunits);
-            ta.ntasks = guided_tasks(nunits, grid, &ta.nbig) + unit0;  // see enqueue_chained
+            const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ta.ntasks, &ta.nbig);
+            ta.ntasks += unit0;  // see enqueue_chained
             ta.nbig += unit0;
             HIPCHK(hipMemsetD32Async((hipDeviceptr_t)dv.counter[si], (int)unit0, 1, st));
             Launch L;
@@ -554,10 +571,29 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
             else it->second += cnt;
         }
         int dom = load.empty() ? -1 : load[0].first;
-        long double most = -1;
-        for (const auto& p : load)
+        long double most = -1, total = 0;
+        for (const auto& p : load) {
+            total += p.second;
             if (p.second > most) { most = p.second; dom = p.first; }
+        }
         uint64_t* best = dv.best + (size_t)r * kStreams * 2;
+        if (nstreams > 1 && total <= (long double)kConcurrentNonces) {
+            // a small request (config 1's [0, 10^7+1], short server chunks):
+            // its launches are latency-bound, so every segment goes onto the
+            // streams round-robin, ungated, largest first: the host enqueues
+            // a segment every ~25 us, and the largest one should not be the
+            // last to start
+            std::vector<size_t> order(segs.size());
+            for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+            std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+                return segs[a].hi - segs[a].lo > segs[b].hi - segs[b].lo;
+            });
+            for (size_t i : order) {
+                int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], rr++ % nstreams, best);
+                if (rc) return rc;
+            }
+            continue;
+        }
         size_t last_dom = 0;
         for (size_t i = 0; i < segs.size(); ++i)
             if (key(segs[i]) == dom) last_dom = i;
