@@ -551,7 +551,8 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     // are queued on the low-priority streams 1.., gated on stream 0 reaching
     // its last dominant segment: they start together with that launch, get
     // workgroup slots only as its persistent waves retire, and so run in its
-    // tail instead of after it.
+    // tail instead of after it.  Small requests (<= kConcurrentNonces) skip
+    // that order: all their segments run at once on all streams.
     const int nstreams = std::max(1, std::min(ctx->streams, kStreams));
     int rr = 0;
     for (int r = 0; r < n; ++r) {
