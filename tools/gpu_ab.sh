@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box recipe: interleaved A/B (both orders) of two builds on cfg2, a
 # medium d=10 request (2^27 nonces) and cfg3, plus a GPU-suite subset on the
-# current build.  usage: tools/gpu_r02_ab4.sh <outdir> <libA> <libB>
+# current build.  usage: tools/gpu_ab.sh <outdir> <libA> <libB>
 set -o pipefail
 export TMPDIR=/tmp
 O=$1; A=$2; B=$3; mkdir -p $O
