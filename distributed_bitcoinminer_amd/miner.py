@@ -7,7 +7,7 @@ The scan itself -- the reference's hot loop, miner.go:46-59 -- runs on the
 GPU through ``hm_scan``.  The reference's ``upper := Upper+1`` (:52) is a
 uint64 add, so ``Upper == 2^64-1`` scans nothing and yields
 ``(MaxUint64, 0)``; that quirk (SURVEY A-inv-5) is reproduced here, in the
-caller, exactly as the Go shim in go/hipminer does it.
+caller, exactly as the Go shim in go/src/hipminer does it.
 
 There is no CPU fallback: if the GPU path fails, ``HipMinerError`` propagates
 and the miner process ends, as the reference miner does on an LSP error

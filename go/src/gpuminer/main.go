@@ -4,7 +4,9 @@
 // libhipminer.so through package hipminer.
 //
 // Usage: gpuminer <host:port>     (HIPMINER_DEVICES=0,1,... selects GPUs)
-// Build in the reference's GOPATH with this repo's go/ directory on it.
+// Build (GOPATH mode: the reference's p1/ and this repo's go/ as GOPATH entries):
+//
+//	GO111MODULE=off GOPATH=<reference>/p1:<repo>/go go build gpuminer
 package main
 
 import (

@@ -3,13 +3,17 @@
 // (cmu440/bitcoin/miner/miner.go:46-59, bitcoin.Hash at
 // cmu440/bitcoin/hash.go:13-17).
 //
-// Built only where a Go toolchain exists (none in the build image); the C ABI
-// it binds is tested from Python/ctypes in tests/.
+// GOPATH layout: this repo's go/ directory is a GOPATH entry (go/src/hipminer),
+// next to the reference's p1/ (github.com/cmu440/...).  Go 1.10 (the staff
+// binaries' go1.10.3) or newer; with Go >= 1.11 build with GO111MODULE=off.
+// Built only where a Go toolchain exists (none in the build image):
+// tests/test_cgo_surface.py checks every C.* name used here against
+// include/hipminer.h and compiles and runs the same C calls with gcc.
 package hipminer
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../distributed_bitcoinminer_amd -lhipminer -Wl,-rpath,${SRCDIR}/../../distributed_bitcoinminer_amd
+#cgo CFLAGS: -I${SRCDIR}/../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../distributed_bitcoinminer_amd -lhipminer -Wl,-rpath,${SRCDIR}/../../../distributed_bitcoinminer_amd
 #include <stdlib.h>
 #include "hipminer.h"
 */
@@ -21,6 +25,16 @@ import (
 )
 
 const maxUint64 = ^uint64(0)
+
+// cbytes copies s into C memory for one call (nil for ""; s may hold any
+// byte, NUL included).  The caller frees it with C.free.  Messages are short,
+// so the copy costs nothing next to a scan.
+func cbytes(s string) *C.uint8_t {
+	if len(s) == 0 {
+		return nil
+	}
+	return (*C.uint8_t)(C.CBytes([]byte(s)))
+}
 
 // Error carries an hm_* return code.
 type Error struct{ Code int }
@@ -57,11 +71,8 @@ func Open(devices ...int) (*Miner, error) {
 // inclusive range [lo, hi]; (MaxUint64, 0) when lo > hi.
 func (m *Miner) ScanInclusive(data string, lo, hi uint64) (hash, nonce uint64, err error) {
 	var out C.hm_result
-	var p *C.uint8_t
-	if len(data) > 0 {
-		// Borrowed for the call only; the bytes hold no Go pointers (cgo rules).
-		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
-	}
+	p := cbytes(data)
+	defer C.free(unsafe.Pointer(p))
 	rc := C.hm_scan(m.ctx, p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi), &out)
 	if rc != 0 {
 		return 0, 0, Error{int(rc)}
@@ -81,10 +92,8 @@ type Request struct {
 func (m *Miner) ScanChecked(data string, lo, hi uint64) (hash, nonce, sum, count uint64, err error) {
 	var out C.hm_result
 	var s, c C.uint64_t
-	var p *C.uint8_t
-	if len(data) > 0 {
-		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
-	}
+	p := cbytes(data)
+	defer C.free(unsafe.Pointer(p))
 	rc := C.hm_scan_checked(m.ctx, p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi), &out, &s, &c)
 	if rc != 0 {
 		return 0, 0, 0, 0, Error{int(rc)}
@@ -109,12 +118,8 @@ func (m *Miner) ScanMany(reqs []Request) ([][2]uint64, error) {
 		}
 	}()
 	for i, r := range reqs {
-		var p *C.uint8_t
-		if len(r.Data) > 0 {
-			b := C.CBytes([]byte(r.Data))
-			cbufs = append(cbufs, b)
-			p = (*C.uint8_t)(b)
-		}
+		p := cbytes(r.Data)
+		cbufs = append(cbufs, unsafe.Pointer(p))
 		creqs[i] = C.hm_request{msg: p, len: C.size_t(len(r.Data)), lo: C.uint64_t(r.Lo), hi: C.uint64_t(r.Hi)}
 	}
 	outs := make([]C.hm_result, len(reqs))
@@ -149,10 +154,8 @@ func (m *Miner) Close() {
 
 // Hash is bitcoin.Hash(msg, nonce) computed by the library on the host.
 func Hash(msg string, nonce uint64) uint64 {
-	var p *C.uint8_t
-	if len(msg) > 0 {
-		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(msg)))
-	}
+	p := cbytes(msg)
+	defer C.free(unsafe.Pointer(p))
 	return uint64(C.hm_hash(p, C.size_t(len(msg)), C.uint64_t(nonce)))
 }
 
@@ -164,10 +167,8 @@ func Partition(data string, lo, hi uint64, n int) ([][2]uint64, error) {
 	if n <= 0 {
 		return nil, Error{int(C.HM_ERR_INVALID)}
 	}
-	var p *C.uint8_t
-	if len(data) > 0 {
-		p = (*C.uint8_t)(unsafe.Pointer(unsafe.StringData(data)))
-	}
+	p := cbytes(data)
+	defer C.free(unsafe.Pointer(p))
 	bounds := make([]C.uint64_t, 2*n)
 	if rc := C.hm_partition(p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi),
 		C.int(n), &bounds[0]); rc != C.HM_OK {

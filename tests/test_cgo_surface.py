@@ -1,0 +1,217 @@
+"""The Go side of the boundary without a Go toolchain (none in this image):
+the cgo binding go/src/hipminer and the miner command go/src/gpuminer
+(they replace cmu440/bitcoin/miner/miner.go:46-59).
+
+What can be checked here, and is:
+* GOPATH layout: go/ is a GOPATH entry, so the import "hipminer" resolves to
+  go/src/hipminer; every non-standard import is that package or the
+  reference's github.com/cmu440/{bitcoin,lsp};
+* the #cgo directives resolve (from ${SRCDIR}) to include/hipminer.h and the
+  in-tree libhipminer.so;
+* every C.<name> the binding uses is a cgo builtin or declared by the header,
+  every C.hm_* call passes as many arguments as the C prototype takes, and
+  the hm_request composite literal names real fields;
+* the binding's preamble, followed by a C replay of the binding's calls with
+  the C types the Go code declares, compiles with gcc -Wall -Werror, links
+  against libhipminer.so and runs the host-only entry points (hm_hash against
+  the golden KATs, hm_partition, hm_strerror, hm_open failing cleanly without
+  a GPU).
+Not checked: Go syntax and type-checking (needs `go build`)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from distributed_bitcoinminer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOPATH = os.path.join(ROOT, "go")
+BINDING = os.path.join(GOPATH, "src", "hipminer", "hipminer.go")
+COMMAND = os.path.join(GOPATH, "src", "gpuminer", "main.go")
+
+CGO_BUILTINS = {"GoString", "GoStringN", "GoBytes", "CString", "CBytes", "malloc", "free",
+                "int", "uint", "char", "size_t", "uint8_t", "uint32_t", "uint64_t", "int64_t"}
+GO_STD = {"encoding/json", "fmt", "os", "strconv", "strings", "unsafe", "errors", "sync"}
+
+
+def _read(p):
+    with open(p) as f:
+        return f.read()
+
+
+def _imports(src):
+    m = re.search(r"^import \((.*?)^\)", src, re.S | re.M)
+    block = m.group(1) if m else ""
+    single = re.findall(r'^import "([^"]+)"', src, re.M)
+    return re.findall(r'"([^"]+)"', block) + single
+
+
+def _preamble(src):
+    m = re.search(r"/\*(.*?)\*/\s*import \"C\"", src, re.S)
+    assert m, "no cgo preamble"
+    return m.group(1)
+
+
+def _header():
+    return _read(_lib.HEADER_PATH)
+
+
+def _c_prototypes():
+    """name -> parameter count of every function include/hipminer.h declares."""
+    protos = {}
+    for m in re.finditer(r"^[\w\s\*]*?\b(hm_\w+)\s*\(([^)]*)\)\s*;", _header(), re.M):
+        params = m.group(2).strip()
+        protos[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return protos
+
+
+def _call_args(src, start):
+    """Top-level argument count of the call whose '(' is at src[start]."""
+    depth, n, i, nonempty = 0, 1, start, False
+    while True:
+        ch = src[i]
+        if ch in "([{":
+            depth += 1
+        elif ch in ")]}":
+            depth -= 1
+            if depth == 0:
+                return n if nonempty else 0
+        elif ch == "," and depth == 1:
+            n += 1
+        elif not ch.isspace() and depth >= 1:
+            nonempty = True
+        i += 1
+
+
+def test_gopath_layout_and_imports():
+    for path in (BINDING, COMMAND):
+        assert os.path.exists(path), path
+    assert re.search(r"^package hipminer$", _read(BINDING), re.M)
+    cmd = _read(COMMAND)
+    assert re.search(r"^package main$", cmd, re.M)
+    for imp in _imports(cmd) + _imports(_read(BINDING)):
+        if imp in GO_STD or imp == "C":
+            continue
+        if imp.startswith("github.com/cmu440/"):
+            assert imp in ("github.com/cmu440/bitcoin", "github.com/cmu440/lsp"), imp
+            continue
+        assert os.path.isdir(os.path.join(GOPATH, "src", imp)), f"import {imp!r} not on GOPATH"
+
+
+def test_cgo_directives_resolve():
+    pre = _preamble(_read(BINDING))
+    srcdir = os.path.dirname(BINDING)
+    flags = " ".join(re.findall(r"#cgo (?:CFLAGS|LDFLAGS):(.*)", pre)).replace("${SRCDIR}", srcdir)
+    incs = re.findall(r"-I(\S+)", flags)
+    libdirs = re.findall(r"-L(\S+)", flags)
+    assert any(os.path.exists(os.path.join(d, "hipminer.h")) for d in incs), incs
+    assert "-lhipminer" in flags
+    assert any(os.path.samefile(os.path.join(d, "libhipminer.so"), _lib.LIB_PATH)
+               for d in libdirs if os.path.exists(os.path.join(d, "libhipminer.so"))), libdirs
+
+
+def test_every_c_name_is_declared_and_calls_match_arity():
+    src = _read(BINDING)
+    hdr = _header()
+    protos = _c_prototypes()
+    names = set(re.findall(r"\bC\.(\w+)", src))
+    assert {"hm_open", "hm_scan", "hm_scan_many", "hm_scan_checked", "hm_partition",
+            "hm_hash", "hm_close", "hm_strerror"} <= names
+    for n in sorted(names - CGO_BUILTINS):
+        declared = n in protos or re.search(rf"(\btypedef struct {n}\b|}} {n};|^#define {n}\b)", hdr, re.M)
+        assert declared, f"C.{n} is not declared by include/hipminer.h"
+    for m in re.finditer(r"\bC\.(hm_\w+)\(", src):
+        name = m.group(1)
+        if name in protos:
+            got = _call_args(src, m.end() - 1)
+            assert got == protos[name], f"C.{name}: {got} args, prototype takes {protos[name]}"
+    # the request literal names hm_request's fields
+    lit = re.search(r"C\.hm_request\{([^}]*)\}", src)
+    assert lit
+    fields = re.findall(r"(\w+):", lit.group(1))
+    body = re.search(r"typedef struct hm_request \{(.*?)\} hm_request;", hdr, re.S).group(1)
+    for f in fields:
+        assert re.search(rf"\b{f}\b\s*[;,]", body), f"hm_request has no field {f}"
+
+
+REPLAY = r"""
+#include <stdio.h>
+#include <string.h>
+
+/* The binding's calls, with the C types its Go code declares. */
+static const char *gostring(int rc) { return hm_strerror(rc); }          /* Error.Error */
+
+int main(int argc, char **argv) {
+    /* Hash(msg, nonce): cbytes(msg) then hm_hash */
+    const char *msg = argv[1];
+    size_t len = strlen(msg);
+    uint8_t *p = len ? (uint8_t *)malloc(len) : NULL;
+    if (p) memcpy(p, msg, len);
+    uint64_t nonce = strtoull(argv[2], NULL, 10);
+    printf("hash %llu\n", (unsigned long long)hm_hash(p, (size_t)len, (uint64_t)nonce));
+
+    /* Partition(data, lo, hi, n) */
+    int n = 8;
+    uint64_t *bounds = (uint64_t *)malloc(sizeof(uint64_t) * 2 * n);
+    int rc = hm_partition(p, (size_t)len, (uint64_t)0, (uint64_t)((1ull << 40) - 1), (int)n,
+                          &bounds[0]);
+    printf("partition %d", rc);
+    for (int i = 0; i < 2 * n; ++i) printf(" %llu", (unsigned long long)bounds[i]);
+    printf("\n");
+    if (hm_partition(p, (size_t)len, 0, 1, 0, &bounds[0]) != HM_ERR_INVALID) return 3;
+
+    /* Open(devices...): both forms; no GPU here -> HM_ERR_NO_DEVICE */
+    hm_ctx *ctx = NULL, *all = NULL;
+    int ds[1] = {0};
+    int rc0 = hm_open(NULL, 0, &all);
+    if (rc0 == HM_OK) hm_close(all);
+    int rc1 = hm_open(&ds[0], (int)1, &ctx);
+    printf("open %d %d %s\n", rc0, rc1, gostring(rc1));
+
+    /* the rest of the surface, type-checked here and only called with a
+       context the GPU run would have opened */
+    hm_result out;
+    uint64_t s, c;
+    hm_request *creqs = (hm_request *)malloc(sizeof(hm_request) * 1);
+    creqs[0] = (hm_request){.msg = p, .len = (size_t)len, .lo = (uint64_t)0, .hi = (uint64_t)9};
+    hm_result outs[1];
+    if (ctx) {
+        rc = hm_scan(ctx, p, (size_t)len, (uint64_t)0, (uint64_t)9, &out);
+        rc = hm_scan_checked(ctx, p, (size_t)len, (uint64_t)0, (uint64_t)9, &out, &s, &c);
+        rc = hm_scan_many(ctx, &creqs[0], (int)1, &outs[0]);
+        hm_close(ctx);
+    }
+    free(creqs);
+    free(bounds);
+    free(p);
+    return 0;
+}
+"""
+
+
+def test_preamble_and_call_replay_compile_link_and_run(tmp_path, golden):
+    pre = _preamble(_read(BINDING))
+    srcdir = os.path.dirname(BINDING)
+    flags = {k: v.replace("${SRCDIR}", srcdir).split()
+             for k, v in re.findall(r"#cgo (CFLAGS|LDFLAGS):(.*)", pre)}
+    includes = "\n".join(l for l in pre.splitlines() if l.startswith("#include"))
+    src = tmp_path / "replay.c"
+    src.write_text(includes + "\n" + REPLAY)
+    exe = tmp_path / "replay"
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                    *flags["CFLAGS"], "-o", str(exe), str(src), *flags["LDFLAGS"]], check=True)
+    kat = next(k for k in golden["hash_kats"] if bytes.fromhex(k["msg_hex"]) == b"bradfitz")
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", ""))
+    r = subprocess.run([str(exe), "bradfitz", kat["nonce"]], capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    lines = dict(l.split(" ", 1) for l in r.stdout.strip().splitlines())
+    assert int(lines["hash"]) == int(kat["hash"])
+    rc, *b = [int(x) for x in lines["partition"].split()]
+    assert rc == 0
+    assert b == [x for pair in _lib.partition(b"bradfitz", 0, (1 << 40) - 1, 8) for x in pair]
+    rc0, rc1, why = lines["open"].split(" ", 2)
+    import torch
+    if not torch.cuda.is_available():
+        assert int(rc0) == int(rc1) == _lib.HM_ERR_NO_DEVICE and why
