@@ -1,4 +1,4 @@
-"""N>1 path on CPU: world_size-2 gloo ranks shard the range and all-gather the
+"""N>1 path on CPU: world_size-2, 3 and 8 gloo ranks shard the range and all-gather the
 16-byte candidates; the merged answer equals the single-range scan.  The GPU
 scan is replaced by the CPU oracle here (test double)."""
 import os
@@ -36,7 +36,7 @@ def _worker(rank, world, port, q):
     q.put((rank, out))
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_distributed_scan(oracle_mod, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
