@@ -107,30 +107,45 @@ DEV void tiled_body(const TiledArgs& A) {
         const uint64_t nbase = (A.tile0 + tile) * A.pow10V + (uint64_t)v * 100u;
         const uint32_t s0X1 = ssig0<false>(X1);  // lane part of sigma0(W[W1])
 
+        // only W[W1] changes from one t0 step to the next
+        constexpr uint32_t VM = 1u << W1;
         for (uint32_t t1 = t1_begin; t1 < t1_end; ++t1) {
+            uint32_t mw[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) mw[k] = W[k];
+            if constexpr (L3) mw[W1 - 2] = Xm2;
+            // loop digits: wave-uniform, in bytes that are zero in X1
+            uint32_t Lt1;
+            if constexpr (STRADDLE) {
+                // last digit opens W[W1], the tens digit closes W[W1-1]
+                mw[W1 - 1] = X0 + (0x30u + t1);
+                Lt1 = 0;
+            } else {
+                mw[W1 - 1] = X0;
+                Lt1 = (0x30u + t1) << 8;
+            }
+            // rounds before W[W1] and round W1 without its loop digits: per
+            // t1.  Round W1 in closed form: T1 = P + L with P invariant in the
+            // t0 loop, so e and a each cost one add of the uniform L there
+            // (the empty asm keeps d + P and P + T2 as the two hoisted sums;
+            // else P + L is shared and costs a third add per nonce).
+            State s1{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
+            sha_rounds_range<VM, W1, 0, W1>(s1, mw, 0);
+            const uint32_t P = s1.h + bsig1<false>(s1.e) + ch(s1.e, s1.f, s1.g) + (kK[W1] + X1);
+            const uint32_t T2 = bsig0<false>(s1.a) + maj(s1.a, s1.b, s1.c);
+            uint32_t dP = s1.d + P, PT = P + T2;
+            asm volatile("" : "+v"(dP), "+v"(PT));
             for (uint32_t t0 = 0; t0 < 10; ++t0) {
                 uint32_t m[16];
 #pragma unroll
-                for (int k = 0; k < 16; ++k) m[k] = W[k];
-                if constexpr (L3) m[W1 - 2] = Xm2;
-                // loop digits: wave-uniform, in bytes that are zero in X1
-                uint32_t L;
-                if constexpr (STRADDLE) {
-                    // last digit opens W[W1], the tens digit closes W[W1-1]:
-                    // work on W[W1-1] depends on t1 only and is hoisted out
-                    // of the t0 loop
-                    m[W1 - 1] = X0 + (0x30u + t1);
-                    L = (0x30u + t0) << 24;
-                } else {
-                    m[W1 - 1] = X0;
-                    L = (((0x30u + t1) << 8) | (0x30u + t0)) << A.loop_shift;
-                }
-                m[W1] = X1 | L;
-                // only W[W1] changes from one t0 step to the next
-                constexpr uint32_t VM = 1u << W1;
+                for (int k = 0; k < 16; ++k) m[k] = mw[k];
+                const uint32_t L = STRADDLE ? (0x30u + t0) << 24 : (Lt1 | (0x30u + t0)) << A.loop_shift;
+                // X1 and L are bit-disjoint: | is +
+                m[W1] = X1 + L;
                 const uint32_t s0w = s0X1 ^ A.s0_loop[t1 * 10u + t0];  // scalar load
-                State s{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7]};
-                sha_rounds<VM, W1>(s, m, s0w);
+                // the state after round W1: a = T1 + T2, e = d + T1
+                State s{PT + L, s1.a, s1.b, s1.c, dP + L, s1.e, s1.f, s1.g};
+                sha_rounds_range<VM, W1, W1 + 1, 64>(s, m, s0w);
                 uint32_t h0, h1;
                 if constexpr (TRAILER) {
                     State o{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],

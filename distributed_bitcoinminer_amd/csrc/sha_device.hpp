@@ -102,9 +102,15 @@ DEV void round_step(State& s, uint32_t m[16], uint32_t s0w) {
     s.d = s.c; s.c = s.b; s.b = s.a; s.a = t1 + t2;
 }
 
-template <uint32_t VM, int SW, int... I>
+template <uint32_t VM, int SW, int FROM = 0, int... I>
 DEV void rounds_seq(State& s, uint32_t m[16], uint32_t s0w, std::integer_sequence<int, I...>) {
-    (round_step<VM, SW, I>(s, m, s0w), ...);
+    (round_step<VM, SW, FROM + I>(s, m, s0w), ...);
+}
+
+// Rounds [FROM, TO) only (see sha_rounds).
+template <uint32_t VM, int SW, int FROM, int TO>
+DEV void sha_rounds_range(State& s, uint32_t m[16], uint32_t s0w = 0) {
+    rounds_seq<VM, SW, FROM>(s, m, s0w, std::make_integer_sequence<int, TO - FROM>{});
 }
 
 // 64 rounds from state s over message m (m is clobbered into the schedule

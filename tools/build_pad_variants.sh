@@ -5,14 +5,14 @@
 # (build/hipminer/scan_kernels.aligned.s).  The 8-byte multiple keeps every
 # hot-loop VALU op at 4 mod 8 (align_loops.py) and moves the loops' offset
 # within the 64/128-B instruction-cache lines.  Output:
-# build/ab_pad/<k>/libhipminer.so, for tools/ab_libs.py on the GPU box.
+# ${PAD_OUT:-build/ab_pad}/<k>/libhipminer.so, for tools/ab_libs.py on the GPU box.
 # usage: tools/build_pad_variants.sh 0 1 2 ...   (after a normal build)
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 B=$ROOT/build/hipminer
 LLVM=/opt/rocm/lib/llvm/bin
 for k in "$@"; do
-    D=$ROOT/build/ab_pad/$k
+    D=$ROOT/${PAD_OUT:-build/ab_pad}/$k
     mkdir -p $D
     python3 - "$B/scan_kernels.aligned.s" "$D/scan.s" "$k" <<'EOF'
 import re, sys
