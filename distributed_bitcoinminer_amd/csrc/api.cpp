@@ -982,7 +982,7 @@ int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
 }
 
 // ---- debug exports for host-side tests (not part of include/hipminer.h) ----
-// Writes up to `cap` segment descriptors as 9 x int64:
+// Writes up to `cap` segment descriptors as 10 x int64:
 //   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces), lane3
 int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
                   int64_t* outv, int cap) {
