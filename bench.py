@@ -293,6 +293,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(cdev)
 
+    if dist is not None:
+        # communicator set-up (RCCL connects its rings on the first
+        # collective): one untimed all-gather of the candidate buffer, so a
+        # run with --warmup 0 does not time connection set-up as scan work
+        cand.zero_()
+        dist.all_gather_into_tensor(gathered, cand)
+        barrier()
+
     def measure(m, lo, hi, steps, warmup):
         """W untimed + K timed steps of (this rank's hm_scan, all-gather of
         the 16-B candidates, min); returns (max-over-ranks seconds, result,
