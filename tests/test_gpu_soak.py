@@ -1,0 +1,58 @@
+"""Randomised parity soak of the HIP path against the C oracle (opt-in).
+
+Runs only when HM_SOAK_SECONDS is set (the default GPU suite skips it): for
+that many seconds, random (message, range) cases through hm_scan_checked,
+each compared with oracle_scan_sum -- the min (hash, nonce) of the reference
+loop (miner.go:46-59 over hash.go:13-17), the sum of every key mod 2^64 and
+the count.  Messages are 0..200 random bytes (any value), ranges sit around
+random digit-count boundaries or anywhere, from 1 to ~2*10^6 nonces, some
+ending at 2^64-1.  HM_SOAK_SEED picks the sequence; a failure names its case.
+Progress goes to stdout every ~10 s (run with -s).
+"""
+import os
+import random
+import time
+
+import pytest
+
+MAX = (1 << 64) - 1
+
+
+def _case(rng):
+    L = rng.choice([rng.randrange(0, 201), rng.randrange(40, 70), rng.randrange(110, 130)])
+    m = bytes(rng.randrange(256) for _ in range(L))
+    span = rng.choice([1, rng.randrange(1, 100), rng.randrange(100, 70_000),
+                       rng.randrange(70_000, 2_000_000)])
+    kind = rng.randrange(4)
+    if kind == 0:  # across a digit-count boundary
+        c = 10 ** rng.randrange(1, 20)
+        lo = max(0, c - rng.randrange(0, span + 1))
+    elif kind == 1:  # near the top of the nonce space
+        lo = MAX - rng.randrange(0, span + 1)
+    else:  # anywhere
+        lo = rng.randrange(0, MAX)
+    hi = min(MAX, lo + span - 1)
+    return m, lo, hi
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.environ.get("HM_SOAK_SECONDS"), reason="opt-in soak (HM_SOAK_SECONDS)")
+@pytest.mark.timeout(3600)
+def test_random_soak_checked(ctx, oracle_mod):
+    budget = float(os.environ["HM_SOAK_SECONDS"])
+    seed = int(os.environ.get("HM_SOAK_SEED", "355"))
+    rng = random.Random(seed)
+    t0 = last = time.time()
+    n = nonces = 0
+    while time.time() - t0 < budget:
+        m, lo, hi = _case(rng)
+        got = ctx.scan_checked(m, lo, hi)
+        exp = oracle_mod.c_scan_sum(m, lo, hi)
+        assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi)
+        n += 1
+        nonces += hi - lo + 1
+        if time.time() - last > 10:
+            last = time.time()
+            print(f"soak: {n} cases, {nonces} nonces, {last - t0:.0f} s", flush=True)
+    print(f"soak done: seed {seed}, {n} cases, {nonces} nonces, all equal to the oracle", flush=True)
+    assert n > 0
