@@ -17,7 +17,9 @@ for w in shapes:
         for line in open(f):
             if line.startswith("{"):
                 r = json.loads(line)
-                g = r["lib"].split("/")[-3]
+                parts = r["lib"].split("/")
+                # build/<group>/<k>/lib.so (offset variants) or build/ab_flags/<name>/lib.so
+                g = parts[-3] if parts[-2].isdigit() else parts[-2]
                 dom[g].append(r["median_dom_GHs"])
                 wall[g].append(r["median_wall_GHs"])
     groups = sorted(dom)
