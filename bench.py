@@ -15,11 +15,20 @@ step of the north star.  Per-GPU work is fixed as N grows: weak scaling.
 value = nonces scanned by all ranks / time, in GH/s.  Inputs live on the GPU
 (the only host input is the 8-byte message); the timed region covers the
 whole hm_scan call (planning, all launches, the 16-B readback) and the merge.
+`ranks` reports each rank's own time and GPU busy time (spread across GPUs).
+
+Secondary workloads of the default run, under `workloads`: cfg3 (BASELINE
+configs[2], the 120-B message on the same weak shards, 5 steps) and cfg4
+(configs[3]: [0, 2^40) split over the N ranks by hm_partition -- strong
+scaling, the configuration of the >= 7.5x target -- 1 step), each checked
+against its oracle fixture.
 
 roofline: INT32 VALU, SURVEY §8(d): algorithmic work = 1552 lane-ops per
 SHA-256 compression x C compressions per nonce; achieved = that work in the
 dominant scan launch / its HIP-event duration (measured live, on the stream
 the kernel runs on); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
+`frac_rounds` prices instead the rounds and schedule words the kernel's
+formulation executes per nonce (rounds_ops_per_nonce).
 cpu_baseline: the reference miner fleet restated on the host -- one thread
 per core of this process's CPU share (<= 16), each a sequential miner over
 its own chunk, running the C restatement of the reference loop
@@ -38,6 +47,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PER_GPU = 1 << 32
+MAXU64 = (1 << 64) - 1
 
 
 def long120() -> bytes:
@@ -93,14 +103,15 @@ def fixture_check(msg: bytes, lo: int, hi: int, res):
 
 
 def code_object_sha16():
-    """sha256 (16 hex) of the scan kernels' code object this tree built
-    (build/hipminer/hipminer_scan.hsaco, embedded in libhipminer.so)."""
-    import hashlib
-    path = os.path.join(ROOT, "build", "hipminer", "hipminer_scan.hsaco")
-    if not os.path.exists(path):
+    """sha256 (16 hex) of the scan kernels' code object embedded in the
+    libhipminer.so this process loaded (the bytes hipModuleLoadData gets), so a
+    PMC summary is matched to the build that actually runs; None if the
+    library cannot be loaded."""
+    try:
+        from distributed_bitcoinminer_amd import _lib
+        return _lib.code_object_sha16()
+    except Exception:
         return None
-    with open(path, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def profiled(kernel: str):
@@ -174,14 +185,64 @@ def cpu_baseline(msg: bytes, name: str):
                              "sample": f"[0, {n1}) on 1 thread, {d1:.2f} s"}}
 
 
+ROUND_OPS = 16      # lane-ops per SHA-256 round
+SCHED_OPS = 11      # ... per message-schedule word (64 x 16 + 48 x 11 = 1552)
+
+
+def _sched_deps(varying):
+    """Schedule words W16..W63 that depend on any message word in `varying`
+    (W[t] = s1(W[t-2]) + W[t-7] + s0(W[t-15]) + W[t-16])."""
+    dep = [i in varying for i in range(64)]
+    for t in range(16, 64):
+        dep[t] = dep[t - 2] or dep[t - 7] or dep[t - 15] or dep[t - 16]
+    return {t for t in range(16, 64) if dep[t]}
+
+
+def rounds_ops_per_nonce(seg, c_eff):
+    """Lane-ops per nonce that the segment's kernel formulation executes,
+    priced at SURVEY's 16 per round and 11 per schedule word, with the work
+    it hoists out of the per-nonce loop amortised over the nonces it serves
+    (DESIGN.md §5 "frac_rounds").
+
+    tiled (hm_tiled_kernel<W1, S, T>): rounds 0..W1 run once per tens digit
+      (10 nonces), round W1 then costs 2 adds per nonce (closed form), rounds
+      W1+1..63 per nonce; schedule words that depend on the loop word W[W1]
+      per nonce, those that depend on the straddled tens digit in W[W1-1] per
+      10 nonces, the rest once per task (100 nonces); a constant trailer
+      block is 64 table-driven rounds per nonce.
+    chained: the final block's schedule is wave-uniform (the K+W table), so
+      64 rounds per nonce, plus the per-lane block 0 (a full 1552) c_eff - 1
+      times per nonce (counted exactly by the library), plus the table build
+      (48 schedule words + 64 K adds per row, 10^f rows per segment).
+    generic: 1552 per compression."""
+    kind = seg["kind"]
+    if kind == 2:  # tiled
+        W1 = seg["W1"]
+        loop = _sched_deps({W1})
+        t1 = _sched_deps({W1 - 1}) - loop if seg["straddle"] else set()
+        rest = 48 - len(loop) - len(t1)
+        ops = (63 - W1) * ROUND_OPS + 2 + (W1 + 1) * ROUND_OPS / 10
+        ops += len(loop) * SCHED_OPS + len(t1) * SCHED_OPS / 10 + rest * SCHED_OPS / 100
+        if seg["trailer"]:
+            ops += 64 * ROUND_OPS
+        return ops, 0.0
+    if kind == 3:  # chained; the table build is returned per segment
+        ops = 64 * ROUND_OPS + OPS_PER_COMPRESSION * (c_eff - 1.0)
+        return ops, 10 ** seg["f"] * (48 * SCHED_OPS + 64)
+    return OPS_PER_COMPRESSION * max(1, c_eff), 0.0
+
+
 def roofline(st, msg, lo, hi):
     """Roofline object of the dominant scan kernel of the last hm_scan (st =
     hm_stats).  achieved = algorithmic ops per launch / average launch time
     (HIP events on the launch stream).  `frac` prices the compressions per
     nonce the kernel executes (dom_compressions_eff: the chained kernel of a
     two-block tail hoists block 0 out of its loop, SURVEY §8(d) "fraction at
-    C = 1"); `frac_algorithmic_C` prices SURVEY's 1552*C with C counted
-    before any hoisting (equal for one-block tails)."""
+    C = 1") at SURVEY's 1552 lane-ops each; `frac_algorithmic_C` prices
+    SURVEY's 1552*C with C counted before any hoisting (equal for one-block
+    tails); `frac_rounds` prices the rounds and schedule words the kernel's
+    formulation executes (rounds_ops_per_nonce: no credit for schedule work a
+    wave-uniform table or a hoist replaces)."""
     from distributed_bitcoinminer_amd import _lib
     C = st["dom_compressions"]
     C_eff = st["dom_compressions_eff"] or C
@@ -192,10 +253,23 @@ def roofline(st, msg, lo, hi):
     achieved_alg = nonces_pl * OPS_PER_COMPRESSION * C / (avg_ms * 1e-3) / 1e12
     traffic_pn, f_eff, valu_pmc, traffic_src = profiled(st["dom_kernel"])
     traffic = round(traffic_pn * nonces_pl) if traffic_pn is not None else None
+    # the dominant kernel's segments (one instantiation may serve several)
+    segs = _lib.debug_plan(msg, lo, hi)
+    dom_seg = max(segs, key=lambda s: s["hi"] - s["lo"])
+    dom_segs = [s for s in segs if (s["kind"], s["W1"], s["straddle"], s["trailer"]) ==
+                (dom_seg["kind"], dom_seg["W1"], dom_seg["straddle"], dom_seg["trailer"])]
+    if dom_seg["kind"] == 3:
+        dom_segs = [s for s in segs if s["kind"] == 3]
+    rops, table = 0.0, 0.0
+    for sg in dom_segs:
+        o, t = rounds_ops_per_nonce(sg, C_eff)
+        rops += o * (sg["hi"] - sg["lo"] + 1)
+        table += t
+    rops = (rops + table) / max(1, sum(s["hi"] - s["lo"] + 1 for s in dom_segs))
+    achieved_rounds = nonces_pl * rops / (avg_ms * 1e-3) / 1e12
     # algorithmic HBM bytes of one dominant launch: its 128-B tile records
     # (10^V nonces each) + one 16-B candidate per wave of the grid; the
     # work queue adds one device-scope atomicAdd per dequeued task
-    dom_seg = max(_lib.debug_plan(msg, lo, hi), key=lambda s: s["hi"] - s["lo"])
     tiles_pl = -(-int(nonces_pl) // 10 ** dom_seg["V"])
     algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
     tasks_pl = int(nonces_pl) // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
@@ -205,6 +279,8 @@ def roofline(st, msg, lo, hi):
             "compressions_per_nonce": round(C_eff, 6),
             "frac_algorithmic_C": round(achieved_alg / PEAK_TOPS, 4),
             "compressions_per_nonce_algorithmic": C,
+            "frac_rounds": round(achieved_rounds / PEAK_TOPS, 4),
+            "ops_per_nonce_rounds": round(rops, 2),
             "traffic": traffic,
             "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
@@ -212,8 +288,7 @@ def roofline(st, msg, lo, hi):
             "queue_atomics_per_launch": tasks_pl,
             "traffic_note": "PMC traffic is the work queue's device-scope atomics "
                             "(one per dequeued task, executed memory-side), not "
-                            "re-reads; cutting them 4x cut WRITE_SIZE 4x but cost "
-                            "kernel rate (DESIGN.md §9)",
+                            "re-reads (DESIGN.md §9)",
             "f_eff_ghz": f_eff,
             "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
             "kernel": st["dom_kernel"],
@@ -241,8 +316,12 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--secondary", default="cfg3,cfg4",
+                    help="comma list of workloads timed after the primary cfg2 run and "
+                         "reported under `workloads` (cfg3: weak, 5 steps; cfg4: strong "
+                         "[0, 2^40), 1 step)")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the secondary cfg3 measurement of the default cfg2 run")
+                    help="skip the secondary measurements of the default cfg2 run")
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="cfg2")
     args = ap.parse_args()
     msg, desc = WORKLOADS[args.workload]
@@ -261,7 +340,7 @@ def main():
     import numpy as np
     import torch
     from distributed_bitcoinminer_amd import _lib
-    from distributed_bitcoinminer_amd.parallel import merge
+    from distributed_bitcoinminer_amd.parallel import merge, shard_range
 
     gpu = local_rank if backend == "nccl" else 0
     dist = None
@@ -293,6 +372,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(cdev)
 
+    def gather_f64(vals):
+        """All ranks' float64 vectors (one all-gather; the bench's only
+        other collective besides the 16-B candidates)."""
+        if dist is None:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        out = torch.empty(world * len(vals), dtype=torch.float64, device=dev)
+        dist.all_gather_into_tensor(out, t)
+        return out.cpu().reshape(world, len(vals)).tolist()
+
     if dist is not None:
         # communicator set-up (RCCL connects its rings on the first
         # collective): one untimed all-gather of the candidate buffer, so a
@@ -302,11 +391,14 @@ def main():
         barrier()
 
     def measure(m, lo, hi, steps, warmup):
-        """W untimed + K timed steps of (this rank's hm_scan, all-gather of
-        the 16-B candidates, min); returns (max-over-ranks seconds, result,
-        rank-0 step times, hm_stats of the last scan)."""
+        """W untimed + K timed steps of (this rank's hm_scan of [lo, hi],
+        all-gather of the 16-B candidates, min).  Returns the max-over-ranks
+        time, the merged result, rank 0's step times, this rank's hm_stats of
+        the last scan and the per-rank timings (each rank's own time to its
+        last result, before the closing barrier, and its summed scan-kernel
+        busy time: DVFS or placement imbalance between GPUs shows there)."""
         def step():
-            local = ctx.scan(m, lo, hi)
+            local = ctx.scan(m, lo, hi) if lo is not None else (MAXU64, 0)
             if dist is None:
                 return local
             cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
@@ -319,49 +411,67 @@ def main():
             res = step()
         barrier()
         t0 = time.perf_counter()
-        step_ms = []
+        step_ms, busy_ms = [], 0.0
         for _ in range(steps):
             ts = time.perf_counter()
             res = step()  # hm_scan returns after its 16-B readback: the step is complete
             step_ms.append((time.perf_counter() - ts) * 1e3)
+            if lo is not None:
+                busy_ms += ctx.stats()["kernel_ms"]
         torch.cuda.synchronize(cdev)
+        local_ms = (time.perf_counter() - t0) * 1e3
         barrier()
         elapsed = time.perf_counter() - t0
-        st = ctx.stats()
-        if dist is not None:
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            elapsed = float(tt.item())
+        st = ctx.stats() if lo is not None else None
+        per_rank = gather_f64([local_ms, busy_ms, elapsed])
+        elapsed = max(r[2] for r in per_rank)
+        loc = [round(r[0], 3) for r in per_rank]
+        ranks = {"local_ms": loc, "kernel_busy_ms": [round(r[1], 3) for r in per_rank],
+                 "local_ms_min": min(loc), "local_ms_max": max(loc),
+                 "spread_pct": round(100.0 * (max(loc) - min(loc)) / max(loc), 3)}
         # self-check: the winner re-hashes to the reported hash (host hm_hash)
         assert _lib.host_hash(m, res[1]) == res[0], res
-        return elapsed, res, step_ms, st
+        return elapsed, res, step_ms, st, ranks
 
-    if args.workload == "cfg4":
-        from distributed_bitcoinminer_amd.parallel import shard_range
-        total_nonces = 1 << 40
-        lo, hi = shard_range(0, total_nonces - 1, world, rank, msg=msg)  # cost-weighted
-    else:
-        total_nonces = world * PER_GPU
-        lo, hi = rank * PER_GPU, (rank + 1) * PER_GPU - 1
-    elapsed, res, step_ms, st = measure(msg, lo, hi, args.steps, args.warmup)
+    def shard_of(name):
+        """(total nonces, this rank's inclusive shard or (None, None)).
+        cfg2/cfg3: weak, rank r scans [r*2^32, (r+1)*2^32); cfg4: strong, the
+        cost-weighted hm_partition shard of [0, 2^40)."""
+        if name == "cfg4":
+            sh = shard_range(0, (1 << 40) - 1, world, rank, msg=WORKLOADS["cfg4"][0])
+            return 1 << 40, sh if sh is not None else (None, None)
+        return world * PER_GPU, (rank * PER_GPU, (rank + 1) * PER_GPU - 1)
+
+    total_nonces, (lo, hi) = shard_of(args.workload)
+    elapsed, res, step_ms, st, ranks = measure(msg, lo, hi, args.steps, args.warmup)
     rl = roofline(st, msg, lo, hi) if rank == 0 else None
 
-    # secondary: BASELINE configs[2] (120-B message, two tail blocks), same
-    # weak-scaling shards, so the driver's run times config 3 as well
-    secondary = None
-    if args.workload == "cfg2" and not args.no_secondary:
-        m3 = long120()
-        steps3 = max(1, min(args.steps, 5))
-        e3, r3, sm3, st3 = measure(m3, lo, hi, steps3, 1)
+    # secondaries of the default cfg2 run, so the driver's run also clocks
+    # BASELINE configs[2] (cfg3: 120-B message, two tail blocks, weak) and
+    # configs[3] (cfg4: [0, 2^40) split over the N ranks, strong scaling --
+    # the configuration the >= 7.5x north-star target is stated on)
+    secondary = {}
+    names = [] if (args.workload != "cfg2" or args.no_secondary) else \
+        [n.strip() for n in args.secondary.split(",") if n.strip()]
+    for name in names:
+        if name not in ("cfg3", "cfg4"):
+            raise SystemExit(f"unknown secondary workload {name!r}")
+        m2 = long120() if name == "cfg3" else WORKLOADS[name][0]
+        tot2, (lo2, hi2) = shard_of(name)
+        steps2, warm2 = (max(1, min(args.steps, 5)), 1) if name == "cfg3" else (1, 0)
+        e2, r2, sm2, st2, rk2 = measure(m2, lo2, hi2, steps2, warm2)
         if rank == 0:
-            secondary = {"cfg3": {
-                "workload": WORKLOADS["cfg3"][1], "value": round(total_nonces * steps3 / e3 / 1e9, 3),
-                "unit": "GH/s", "steps": steps3, "warmup": 1,
-                "ms_per_step": round(e3 / steps3 * 1e3, 3),
-                "ms_per_step_median_rank0": round(sorted(sm3)[len(sm3) // 2], 3),
-                "result": {"hash": r3[0], "nonce": r3[1]},
-                "result_vs_oracle": fixture_check(m3, 0, total_nonces - 1, r3),
-                "roofline": roofline(st3, m3, lo, hi)}}
+            secondary[name] = {
+                "workload": WORKLOADS[name][1], "value": round(tot2 * steps2 / e2 / 1e9, 3),
+                "unit": "GH/s", "scaling": "strong" if name == "cfg4" else "weak",
+                "steps": steps2, "warmup": warm2,
+                "ms_per_step": round(e2 / steps2 * 1e3, 3),
+                "ms_per_step_median_rank0": round(sorted(sm2)[len(sm2) // 2], 3),
+                "nonces_rank0": (hi2 - lo2 + 1) if lo2 is not None else 0,
+                "result": {"hash": r2[0], "nonce": r2[1]},
+                "result_vs_oracle": fixture_check(m2, 0, tot2 - 1, r2),
+                "ranks": rk2,
+                "roofline": roofline(st2, m2, lo2, hi2) if lo2 is not None else None}
 
     if rank == 0:
         total = total_nonces * args.steps
@@ -386,6 +496,7 @@ def main():
                                 if dist is not None else "none (1 rank)"},
             "result": {"hash": res[0], "nonce": res[1]},
             "result_vs_oracle": fixture_check(msg, 0, total_nonces - 1, res),
+            "ranks": ranks,
             "roofline": rl,
         }
         if secondary:

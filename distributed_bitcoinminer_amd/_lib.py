@@ -96,6 +96,11 @@ def load() -> ctypes.CDLL:
                                         ctypes.POINTER(ctypes.c_uint64)]
         lib.hm_scan_stats.restype = ctypes.c_int
         lib.hm_scan_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats)]
+        lib.hm_scan_stats_sized.restype = ctypes.c_int
+        lib.hm_scan_stats_sized.argtypes = [ctypes.c_void_p, ctypes.POINTER(hm_stats),
+                                            ctypes.c_size_t]
+        lib.hm_debug_code_object.restype = ctypes.c_size_t
+        lib.hm_debug_code_object.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
         lib.hm_set_option.restype = ctypes.c_int
         lib.hm_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]
         lib.hm_strerror.restype = ctypes.c_char_p
@@ -181,7 +186,7 @@ class Context:
 
     def stats(self) -> dict:
         st = hm_stats()
-        rc = self._lib.hm_scan_stats(self._h, ctypes.byref(st))
+        rc = self._lib.hm_scan_stats_sized(self._h, ctypes.byref(st), ctypes.sizeof(st))
         if rc != HM_OK:
             raise HipMinerError(rc, "hm_scan_stats")
         return st.as_dict()
@@ -230,15 +235,26 @@ def partition(msg, lo: int, hi: int, n: int) -> list:
     return out
 
 
+def code_object_sha16() -> str:
+    """sha256 (16 hex digits) of the scan kernels' code object embedded in the
+    loaded libhipminer.so (the bytes hipModuleLoadData gets)."""
+    import hashlib
+    p = ctypes.c_void_p()
+    n = load().hm_debug_code_object(ctypes.byref(p))
+    return hashlib.sha256(ctypes.string_at(p.value, n)).hexdigest()[:16]
+
+
 def debug_plan(msg, lo: int, hi: int, force_generic: bool = False) -> list[dict]:
     m = as_bytes(msg)
     cap = 32
-    buf = (ctypes.c_int64 * (10 * cap))()
+    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost", "lane3",
+            "f", "tch")
+    k = len(keys)
+    buf = (ctypes.c_int64 * (k * cap))()
     n = load().hm_debug_plan(m, len(m), lo, hi, int(force_generic), buf, cap)
-    keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost", "lane3")
     out = []
     for i in range(min(n, cap)):
-        row = dict(zip(keys, buf[10 * i: 10 * i + 10]))
+        row = dict(zip(keys, buf[k * i: k * i + k]))
         row["lo"] &= (1 << 64) - 1
         row["hi"] &= (1 << 64) - 1
         out.append(row)

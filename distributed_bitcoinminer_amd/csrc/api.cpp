@@ -38,6 +38,7 @@ using namespace hm;
 
 // The scan kernels' code object (scan_blob.S .incbin of hipminer_scan.hsaco).
 extern "C" const unsigned char hm_scan_code_object[];
+extern "C" const unsigned char hm_scan_code_object_end[];
 
 namespace {
 
@@ -254,12 +255,12 @@ uint32_t count_compressions(const SegPlan& s) {
 
 // Compressions per nonce the segment's scan kernel executes: the algorithmic
 // C minus what is hoisted out of the per-nonce loop (hm_stats.dom_compressions_eff).
+// The chained kernel's launches count their block-0 compressions exactly
+// (one per task and lane, enqueue_chained), guided-split pieces included.
 double executed_compressions(const SegPlan& s) {
     switch (s.kind) {
         case HM_KIND_TILED:  // a two-block tail's block 0 is compressed per tile by the planner
             return s.trailer ? 2.0 : 1.0;
-        case HM_KIND_CHAINED:  // per-lane block 0 once per loop chunk of tch values
-            return 1.0 + 1.0 / (double)s.tch;
         default:
             return (double)s.nb;
     }
@@ -372,6 +373,9 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
         if (rc) return rc;
         const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ca.ntasks, &ca.nbig);
+        // every task compresses its lanes' tail block 0 once; the final block
+        // runs once per lane and loop value: nunits * tch values per lane
+        const double block0_per_value = (double)ca.ntasks / ((double)nunits * (double)s.tch);
         // task ids start at unit0 (the queue counter too): the kernels map a
         // task below nbig to that unit, so the skipped units are never dequeued
         ca.ntasks += unit0;
@@ -387,7 +391,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
         L.grid = grid;
         L.compressions = count_compressions(s);
-        L.comp_eff = executed_compressions(s);
+        L.comp_eff = 1.0 + block0_per_value;
         HIPCHK(hipEventRecord(L.start, st));
         rc = launch_scan(*fn, ca, grid, st);
         if (rc) return rc;
@@ -631,11 +635,16 @@ bool lex_less(uint64_t k1, uint64_t n1, uint64_t k2, uint64_t n2) {
 // All-gather every device's n 16-B results over RCCL; device 0 folds them.
 // Runs for any device count, including one (a 1-rank communicator), so the
 // path the 8-GPU context takes is exercised on a 1-GPU box.
+bool distinct_ordinals(const hm_ctx* ctx) {
+    const size_t n = ctx->devs.size();
+    for (size_t i = 0; i < n; ++i)
+        for (size_t j = 0; j < i; ++j)
+            if (ctx->devs[i].ordinal == ctx->devs[j].ordinal) return false;
+    return true;
+}
+
 int rccl_merge(hm_ctx* ctx, int nreq) {
     const int n = (int)ctx->devs.size();
-    for (int i = 0; i < n; ++i)  // one RCCL rank per device: ordinals must differ
-        for (int j = 0; j < i; ++j)
-            if (ctx->devs[i].ordinal == ctx->devs[j].ordinal) return HM_ERR_INVALID;
     if (!ctx->devs[0].comm) {
         std::vector<ncclComm_t> comms(n);
         std::vector<int> ords(n);
@@ -671,6 +680,9 @@ int rccl_merge(hm_ctx* ctx, int nreq) {
 // One chunk (<= kMaxBatch requests) of hm_scan_many.
 int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, bool first) {
     const int ndev = (int)ctx->devs.size();
+    // one RCCL rank per device (hm_set_option refuses the option otherwise);
+    // checked again here, before any work is enqueued
+    if (ctx->merge_rccl && !distinct_ordinals(ctx)) return HM_ERR_INVALID;
     std::vector<MsgPlan> plans(nreq);
     std::vector<std::vector<DevReq>> per_dev(ndev, std::vector<DevReq>(nreq));
     static const uint8_t empty_msg = 0;
@@ -736,8 +748,9 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
 }
 
 // 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked;
-// 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count
-int hm_version(void) { return (1 << 16) | 4; }
+// 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count;
+// 1.5: hm_scan_stats_sized, HM_OPT_MERGE_RCCL refused up front for repeated ordinals
+int hm_version(void) { return (1 << 16) | 5; }
 
 int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t* bounds) {
@@ -825,7 +838,12 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
     std::lock_guard<std::mutex> g(ctx->mu);
     switch (opt) {
         case HM_OPT_FORCE_GENERIC: ctx->force_generic = value != 0; return HM_OK;
-        case HM_OPT_MERGE_RCCL: ctx->merge_rccl = value != 0; return HM_OK;
+        case HM_OPT_MERGE_RCCL:
+            // RCCL needs one rank per device: a context naming a device twice
+            // can never merge over RCCL, so the option is refused up front
+            if (value != 0 && !distinct_ordinals(ctx)) return HM_ERR_INVALID;
+            ctx->merge_rccl = value != 0;
+            return HM_OK;
         case HM_OPT_STREAMS:
             if (value < 1 || value > kStreams) return HM_ERR_INVALID;
             ctx->streams = (int)value;
@@ -974,16 +992,30 @@ int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, ui
 
 
 int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
-    if (!ctx || !out) return HM_ERR_INVALID;
+    return hm_scan_stats_sized(ctx, out, sizeof(hm_stats));
+}
+
+int hm_scan_stats_sized(const hm_ctx* ctx, hm_stats* out, size_t size) {
+    // a caller built against an older header passes its smaller struct:
+    // only its prefix is written (the layout only ever grows at the end)
+    if (!ctx || !out || size < HM_STATS_SIZE_1_0) return HM_ERR_INVALID;
     std::lock_guard<std::mutex> g(ctx->mu);  // scans write ctx->last under the lock
     if (!ctx->have_stats) return HM_ERR_INVALID;
-    *out = ctx->last;
+    memcpy(out, &ctx->last, std::min(size, sizeof(hm_stats)));
     return HM_OK;
 }
 
 // ---- debug exports for host-side tests (not part of include/hipminer.h) ----
-// Writes up to `cap` segment descriptors as 10 x int64:
-//   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces), lane3
+// The embedded scan code object (scan_blob.S): bench.py hashes these bytes to
+// match a PMC summary to the build that actually runs.
+size_t hm_debug_code_object(const unsigned char** p) {
+    if (p) *p = hm_scan_code_object;
+    return (size_t)(hm_scan_code_object_end - hm_scan_code_object);
+}
+
+// Writes up to `cap` segment descriptors as 12 x int64:
+//   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces), lane3,
+//   f (chained: final-block digits), tch (chained: loop values per task)
 int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
                   int64_t* outv, int cap) {
     if (lo > hi) return 0;
@@ -998,11 +1030,13 @@ int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int 
     int i = 0;
     for (; i < (int)segs.size() && i < cap; ++i) {
         const SegPlan& s = segs[i];
-        int64_t* o = outv + 10 * i;
+        int64_t* o = outv + 12 * i;
         o[0] = s.d; o[1] = (int64_t)s.lo; o[2] = (int64_t)s.hi; o[3] = s.kind;
         o[4] = s.W1; o[5] = s.V; o[6] = s.trailer; o[7] = s.straddle;
         o[8] = (int64_t)seg_cost(s);
         o[9] = s.lane3;
+        o[10] = s.kind == HM_KIND_CHAINED ? s.f : 0;
+        o[11] = s.kind == HM_KIND_CHAINED ? s.tch : 0;
     }
     return (int)segs.size();
 }

@@ -9,4 +9,6 @@
 hm_scan_code_object:
     .incbin "hipminer_scan.hsaco"
     .size hm_scan_code_object, . - hm_scan_code_object
+    .globl hm_scan_code_object_end
+hm_scan_code_object_end:
     .section .note.GNU-stack, "", @progbits

@@ -86,10 +86,17 @@ typedef struct hm_stats {
                                   loop.  Tiled: 1 (+1 with a constant trailer
                                   block); chained: 1 + 1/tch, the per-lane block
                                   0 amortised over tch = min(10^f, 1000) loop
-                                  values; generic: dom_compressions.  Mean
-                                  over the dominant kernel's nonces (one
-                                  instantiation may serve several segments). */
+                                  values (counted exactly per launch since ABI
+                                  1.5: one block-0 compression per task and
+                                  lane, guided-split pieces included); generic:
+                                  dom_compressions.  Mean over the dominant
+                                  kernel's nonces (one instantiation may serve
+                                  several segments). */
 } hm_stats;
+
+/* sizeof(hm_stats) by ABI version.  The struct only grows at its end. */
+#define HM_STATS_SIZE_1_0 136 /* ABI 1.0 .. 1.3                                 */
+#define HM_STATS_SIZE_1_4 144 /* ABI 1.4+: + dom_compressions_eff               */
 
 #define HM_MERGE_NONE 0 /* one device: its result is read back directly      */
 #define HM_MERGE_HOST 1 /* several devices: 16-B results merged on the host  */
@@ -114,8 +121,9 @@ typedef struct hm_stats {
 #define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */
 #define HM_OPT_MERGE_RCCL 2    /* 1: merge the per-device candidates with one RCCL
                                   all-gather (also with one device: a 1-rank
-                                  communicator); needs distinct device ordinals,
-                                  else hm_scan* return HM_ERR_INVALID         */
+                                  communicator); needs distinct device ordinals:
+                                  hm_set_option returns HM_ERR_INVALID for a
+                                  context that names a device twice (ABI 1.5)  */
 #define HM_OPT_GRID_PER_CU 3   /* workgroups per CU for scan launches (0 = auto) */
 #define HM_OPT_STREAMS 4       /* HIP streams per device for segment launches
                                   (1..4, default 4): the dominant kernel's
@@ -176,8 +184,16 @@ int hm_scan_checked(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, ui
 int hm_partition(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t *bounds);
 
-/* Stats of the last successful hm_scan / hm_scan_many on ctx. */
+/* Stats of the last successful hm_scan / hm_scan_many on ctx.  Writes
+ * sizeof(hm_stats) of THIS header (HM_STATS_SIZE_1_4 bytes): a caller built
+ * against an older header (136-byte struct, ABI <= 1.3) must use
+ * hm_scan_stats_sized instead, or check hm_version() >= 0x10004 first. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
+
+/* hm_scan_stats writing at most `size` bytes (pass sizeof(hm_stats) as the
+ * caller compiled it; >= HM_STATS_SIZE_1_0): the prefix of the current
+ * layout that fits.  ABI 1.5. */
+int hm_scan_stats_sized(const hm_ctx *ctx, hm_stats *out, size_t size);
 
 int hm_set_option(hm_ctx *ctx, int opt, int64_t value);
 

@@ -64,3 +64,25 @@ def test_roofline_prices_executed_compressions(monkeypatch):
     assert abs(rl["frac_algorithmic_C"] - ghs * 1552 * 2 / 78.6432e12) < 1e-3
     assert rl["compressions_per_nonce"] == 1.001 and rl["compressions_per_nonce_algorithmic"] == 2
     assert _lib.debug_plan(bench.long120(), 0, 2**32 - 1)  # the plan the line reads
+    # frac_rounds: 64 table-driven rounds + the per-lane block 0 + the K+W
+    # tables (10^f rows of 48 schedule words and 64 K adds per segment)
+    segs = [s for s in _lib.debug_plan(bench.long120(), 0, 2**32 - 1) if s["kind"] == 3]
+    n = sum(s["hi"] - s["lo"] + 1 for s in segs)
+    ops = 1024 + 1552 * 0.001 + sum(10 ** s["f"] * (48 * 11 + 64) for s in segs) / n
+    assert abs(rl["ops_per_nonce_rounds"] - ops) < 0.01
+    assert abs(rl["frac_rounds"] - ghs * ops / 78.6432e12) < 1e-3
+
+
+def test_rounds_ops_of_the_tiled_kernel():
+    """cfg2's hm_tiled_kernel<4, false, false>: rounds 0..4 once per tens digit,
+    round 4 then 2 adds per nonce, rounds 5..63 per nonce; the 45 schedule
+    words W19..W63 depend on the loop word W4, W16..W18 once per task."""
+    seg = {"kind": 2, "W1": 4, "straddle": 0, "trailer": 0}
+    ops, table = bench.rounds_ops_per_nonce(seg, 1.0)
+    assert table == 0
+    assert abs(ops - (59 * 16 + 2 + 5 * 16 / 10 + 45 * 11 + 3 * 11 / 100)) < 1e-9
+    assert bench._sched_deps({4}) == set(range(19, 64))
+    # a constant trailer block adds 64 table-driven rounds per nonce
+    ops_t, _ = bench.rounds_ops_per_nonce(dict(seg, W1=14, trailer=1), 2.0)
+    ops_n, _ = bench.rounds_ops_per_nonce(dict(seg, W1=14), 1.0)
+    assert abs(ops_t - ops_n - 64 * 16) < 1e-9

@@ -1,0 +1,75 @@
+"""bench.py's torch.distributed path with the HIP scan underneath, launched the
+way the driver launches it (python -m torch.distributed.run ... bench.py
+--gpus N), on the GPU box:
+
+* 2 ranks with the gloo backend sharing GPU 0 (RCCL refuses two ranks on one
+  device): cfg2 weak scaling ([0, 2 * 2^32)) and the cfg4 secondary (strong
+  scaling: [0, 2^40) as 2 hm_partition shards), each whole-job answer equal to
+  its oracle fixture (tests/golden/full_size.json);
+* 1 rank with the nccl backend (RCCL) and HM_BENCH_FORCE_DIST=1, so the
+  RCCL all-gather of the 16-B candidates runs end to end: cfg2 and the cfg3
+  secondary against tests/golden/large.json.
+
+The reference's split and merge: cmu440/bitcoin/server/server.go:165-205 and
+:273-276.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _torchrun(nproc, args, env_extra, timeout):
+    env = dict(os.environ, **env_extra)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
+           "--nproc-per-node", str(nproc), "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), "bench.py", "--gpus", str(nproc)] + args
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 prints exactly one JSON line
+    return json.loads(lines[0])
+
+
+def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
+    line = _torchrun(2, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
+                         "--no-cpu-baseline"], {"HM_BENCH_BACKEND": "gloo"}, timeout=240)
+    assert line["n_gpus"] == 2 and line["config"]["merge"] == "gloo"
+    assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
+    assert len(line["ranks"]["local_ms"]) == 2
+    c4 = line["workloads"]["cfg4"]
+    assert c4["scaling"] == "strong"
+    assert c4["result_vs_oracle"]["fixture"] == "tests/golden/full_size.json"
+    assert c4["result_vs_oracle"]["match"] is True, c4["result_vs_oracle"]
+    assert len(c4["ranks"]["local_ms"]) == 2 and c4["ranks"]["spread_pct"] >= 0
+    # rank 0's shard is the first hm_partition shard of [0, 2^40)
+    from distributed_bitcoinminer_amd import _lib
+    lo, hi = _lib.partition(b"bradfitz", 0, (1 << 40) - 1, 2)[0]
+    assert c4["nonces_rank0"] == hi - lo + 1
+
+
+def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
+    line = _torchrun(1, ["--steps", "2", "--warmup", "1", "--secondary", "cfg3",
+                         "--no-cpu-baseline"], {"HM_BENCH_FORCE_DIST": "1"}, timeout=180)
+    assert line["config"]["merge"] == "RCCL all-gather"
+    assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
+    c3 = line["workloads"]["cfg3"]
+    assert c3["result_vs_oracle"]["match"] is True, c3["result_vs_oracle"]
+    rl = c3["roofline"]
+    assert rl["kernel"] == "hm_chained_kernel"
+    assert 0 < rl["frac_rounds"] < rl["frac"] <= 1.0

@@ -177,10 +177,38 @@ def test_options_streams_and_rccl_merge(oracle_mod):
     with _lib.Context([0, 0]) as c:  # one RCCL rank per device: duplicates are refused
         assert c.scan(b"jonny greenwood", lo, hi) == exp
         assert c.stats()["merge"] == _lib.HM_MERGE_HOST
-        c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+        # refused where the option is set (ABI 1.5), before any scan work
         with pytest.raises(_lib.HipMinerError) as ei:
-            c.scan(b"jonny greenwood", lo, hi)
+            c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
         assert ei.value.rc == _lib.HM_ERR_INVALID
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        assert c.stats()["merge"] == _lib.HM_MERGE_HOST
+
+
+def test_rccl_merge_distinct_devices(oracle_mod):
+    """The in-library RCCL merge over DISTINCT device ordinals: ncclCommInitAll
+    over every visible GPU, one rank per device, each scanning its
+    hm_partition shard, then the grouped ncclAllGather of the 16-B results and
+    the device-side fold (api.cpp rccl_merge; the multi-device form of
+    server.go:273-276).  Needs >= 2 GPUs: the 1-GPU box skips it."""
+    import torch
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip(f"{n} visible GPU(s): distinct-ordinal RCCL merge needs >= 2")
+    lo, hi = 10**8 - 3_000_000, 10**8 + 3_000_000
+    exp = oracle_mod.c_scan(b"jonny greenwood", lo, hi)
+    ck_lo, ck_hi = 10**9 - 700_000, 10**9 + 500_000
+    exp_ck = oracle_mod.c_scan_sum(b"a" * 45, ck_lo, ck_hi)
+    reqs = [(b"bradfitz", 10**k - 999, 10**k + 4000) for k in range(3, 20)]
+    exp_many = [oracle_mod.c_scan(m, a, b) for m, a, b in reqs]
+    with _lib.Context(list(range(n))) as c:
+        c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+        assert c.scan(b"jonny greenwood", lo, hi) == exp
+        st = c.stats()
+        assert st["merge"] == _lib.HM_MERGE_RCCL and st["ndev"] == n
+        assert c.scan_many(reqs) == exp_many
+        assert c.scan_checked(b"a" * 45, ck_lo, ck_hi) == exp_ck
+        assert c.scan(b"bradfitz", 5, 4) == (MAX, 0)
 
 
 def test_miner_eval_request_on_gpu(ctx, golden):
@@ -208,7 +236,9 @@ def test_stats_accounting(ctx):
     ctx.scan(long120, 10**9, 10**9 + 10**8)
     st = ctx.stats()
     assert st["dom_kind"] == _lib.HM_KIND_CHAINED and st["dom_compressions"] == 2
-    assert st["dom_compressions_eff"] == pytest.approx(1.001)
+    # counted exactly (ABI 1.5): one block-0 compression per task and lane;
+    # whole units cost 1/1000 per loop value, guided-split ones 10/1000
+    assert 1.001 <= st["dom_compressions_eff"] <= 1.01
     # a scan_many batch over several chunks times every launch against one
     # origin: the union of launch intervals is positive and below the wall time
     ctx.scan_many([(b"bradfitz", 10**9 + 10**7 * i, 10**9 + 10**7 * (i + 1) - 1)
