@@ -4,9 +4,11 @@ mix of the innermost loop body (one iteration = 64 nonces per wave for the
 tiled and chained kernels).
 
 usage: make -C distributed_bitcoinminer_amd/csrc asm
-       python tools/isa_audit.py build/hipminer/scan_kernels.aligned.s > profiles/r01/isa_audit.txt
+       python tools/isa_audit.py build/hipminer/scan_kernels.aligned.s > profiles/r03/isa_audit.txt
 (the scan kernels as shipped, after the placement pass align_loops.py)
 
+lane-spill-ops counts the v_writelane/v_readlane instructions SGPR spills
+compile into, in the whole kernel and inside its hot loop.
 model_cyc prices the loop with the measured gfx950 issue costs of DESIGN.md
 §4 (half-rate 4.3, full-rate 2.4 cycles per wave64 instruction: the issue floor
 of the placed hot loops, which the measured kernels reach within ≈1 %).
@@ -49,6 +51,19 @@ def loop_mix(lines, start, end):
     return collections.Counter(ops)
 
 
+def lane_spills(lines, start, end):
+    """(in the hot loop, in the whole kernel) counts of the v_writelane /
+    v_readlane pairs SGPR spills to VGPR lanes compile into."""
+    body = lines[start:end]
+    hdrs = [i for i, l in enumerate(body) if "Inner Loop Header" in l]
+    lane = [i for i, l in enumerate(body) if re.match(r"\s+v_(read|write)lane_b32", l)]
+    if not hdrs:
+        return None, len(lane)
+    hdr = max(hdrs)
+    stop = next((i for i in range(hdr, len(body)) if "s_cbranch_vccz" in body[i]), hdr)
+    return sum(1 for i in lane if hdr <= i < stop), len(lane)
+
+
 def main(path):
     text = open(path).read()
     lines = text.split("\n")
@@ -71,6 +86,9 @@ def main(path):
                f"spills={m['vgpr_spill_count']}/{m['sgpr_spill_count']} "
                f"scratch={m['private_segment_fixed_size']}")
         mix = loop_mix(lines, i0, i1) if ("tiled" in sym or "chained" in sym) else None
+        in_loop, in_kernel = lane_spills(lines, i0, i1)
+        if in_kernel:
+            row += f" lane-spill-ops={in_kernel} (hot loop: {in_loop})"
         if mix:
             n = sum(mix.values())
             half = sum(v for k, v in mix.items() if k.split("_e32")[0] in HALF or k in HALF)
