@@ -25,6 +25,7 @@ HM_ERR_INTERNAL = -6
 
 HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
+HM_OPT_TABLE_DIGITS = 7
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
@@ -248,7 +249,7 @@ def debug_plan(msg, lo: int, hi: int, force_generic: bool = False) -> list[dict]
     m = as_bytes(msg)
     cap = 32
     keys = ("d", "lo", "hi", "kind", "W1", "V", "trailer", "straddle", "cost", "lane3",
-            "f", "tch")
+            "f", "tch", "fe")
     k = len(keys)
     buf = (ctypes.c_int64 * (k * cap))()
     n = load().hm_debug_plan(m, len(m), lo, hi, int(force_generic), buf, cap)

@@ -83,6 +83,7 @@ struct Device {
     hipStream_t stream[kStreams] = {};
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
+    uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
@@ -128,6 +129,7 @@ struct hm_ctx {
     bool merge_rccl = false;
     int grid_per_cu = 0;
     int streams = kStreams;  // HM_OPT_STREAMS (tail filling by default)
+    int table_digits = 0;    // HM_OPT_TABLE_DIGITS (test hook; 0 = default, -1 = off)
     bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
     bool have_stats = false;
     int merge = HM_MERGE_NONE;  // how the current call merged device results
@@ -164,6 +166,7 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
+        dv.kwt_rows[s] = kMaxChainedTable;
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
         HIPCHK(hipMalloc(&dv.sums[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
@@ -328,13 +331,34 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
+// Make stream si's K+W table hold `rows` rows.  Grown once to the largest
+// table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of >= 5 digits); the
+// old table may still be read by work queued earlier on any stream, so the
+// device's streams are drained first.
+int kw_table_rows(Device& dv, int si, uint64_t rows) {
+    if (rows <= dv.kwt_rows[si]) return HM_OK;
+    for (int q = 0; q < kStreams; ++q) HIPCHK(hipStreamSynchronize(dv.stream[q]));
+    HIPCHK(hipFree(dv.kwt[si]));
+    dv.kwt[si] = nullptr;
+    dv.kwt_rows[si] = 0;
+    HIPCHK(hipMalloc(&dv.kwt[si], (size_t)rows * 64 * sizeof(uint32_t)));
+    dv.kwt_rows[si] = rows;
+    return HM_OK;
+}
+
 int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si,
                     uint64_t* best) {
     hipStream_t st = dv.stream[si];
-    HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.total_bits, st));
+    if (s.fe < 1 || s.fe > kMaxTableDigits || s.fe > s.f) return HM_ERR_INTERNAL;
+    const uint64_t nloop = pow10_u64(s.fe);       // table rows = loop values per lane
+    const uint64_t nep = pow10_u64(s.f - s.fe);   // epochs: the final block's high digits
+    int rc = kw_table_rows(dv, si, nloop);
+    if (rc) return rc;
     const uint64_t per_tile = (uint64_t)s.tpt * s.ntc;
     const uint64_t max_tiles = std::min<uint64_t>(kMaxTilesPerLaunch, 0x7fffffffull / per_tile);
-    for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
+    for (uint64_t e = 0; e < nep; ++e) {
+      HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.fe, e * nloop, s.total_bits, st));
+      for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
         const uint64_t nt = std::min<uint64_t>(max_tiles, s.tile_hi - t + 1);
         PlanArgs pa;
         pa.rec = dv.rec[si];
@@ -359,6 +383,8 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.tile0 = t;
         ca.pow10qf = s.pow10V;
         ca.pow10f = pow10_u64(s.f);
+        ca.ebase = e * nloop;
+        ca.nloop = (uint32_t)nloop;
         ca.seg_lo = s.lo;
         ca.seg_hi = s.hi;
         uint32_t unit0;
@@ -370,7 +396,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
         ca.q = s.q;
         const Device::Fn* fn = nullptr;
-        int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
+        rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
         if (rc) return rc;
         const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ca.ntasks, &ca.nbig);
         // every task compresses its lanes' tail block 0 once; the final block
@@ -386,7 +412,9 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         if (rc) return rc;
         rc = next_event(dv, &L.stop);
         if (rc) return rc;
-        L.nonces = tile_span_nonces(s, t, nt);
+        // the epochs split every lane value's nonces evenly (stats only)
+        const uint64_t span = tile_span_nonces(s, t, nt);
+        L.nonces = span / nep + (e + 1 == nep ? span % nep : 0);
         L.kind = HM_KIND_CHAINED;
         snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
         L.grid = grid;
@@ -404,6 +432,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
         dv.launches.push_back(L);
         t += nt;
         if (t == 0) break;
+      }
     }
     return HM_OK;
 }
@@ -562,7 +591,7 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     for (int r = 0; r < n; ++r) {
         if (reqs[r].empty) continue;
         std::vector<SegPlan> segs = plan_range(*reqs[r].mp, reqs[r].lo, reqs[r].hi,
-                                               ctx->force_generic);
+                                               ctx->force_generic, ctx->table_digits);
         // instantiation key per segment, and the key with the most nonces
         auto key = [](const SegPlan& g) {
             return g.kind * 1000 + g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0);
@@ -848,6 +877,10 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
             if (value < 1 || value > kStreams) return HM_ERR_INVALID;
             ctx->streams = (int)value;
             return HM_OK;
+        case HM_OPT_TABLE_DIGITS:
+            if (value < -1 || value > (int64_t)kMaxTableDigits) return HM_ERR_INVALID;
+            ctx->table_digits = (int)value;
+            return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;
             ctx->grid_per_cu = (int)value;
@@ -1013,9 +1046,10 @@ size_t hm_debug_code_object(const unsigned char** p) {
     return (size_t)(hm_scan_code_object_end - hm_scan_code_object);
 }
 
-// Writes up to `cap` segment descriptors as 12 x int64:
+// Writes up to `cap` segment descriptors as 13 x int64:
 //   d, lo, hi, kind, W1, V, trailer, straddle, seg_cost (SIMD cycles / 64 nonces), lane3,
-//   f (chained: final-block digits), tch (chained: loop values per task)
+//   f (chained: final-block digits), tch (chained: loop values per unit),
+//   fe (chained: table digits; f - fe epoch digits)
 int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int force_generic,
                   int64_t* outv, int cap) {
     if (lo > hi) return 0;
@@ -1030,13 +1064,14 @@ int hm_debug_plan(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int 
     int i = 0;
     for (; i < (int)segs.size() && i < cap; ++i) {
         const SegPlan& s = segs[i];
-        int64_t* o = outv + 12 * i;
+        int64_t* o = outv + 13 * i;
         o[0] = s.d; o[1] = (int64_t)s.lo; o[2] = (int64_t)s.hi; o[3] = s.kind;
         o[4] = s.W1; o[5] = s.V; o[6] = s.trailer; o[7] = s.straddle;
         o[8] = (int64_t)seg_cost(s);
         o[9] = s.lane3;
         o[10] = s.kind == HM_KIND_CHAINED ? s.f : 0;
         o[11] = s.kind == HM_KIND_CHAINED ? s.tch : 0;
+        o[12] = s.kind == HM_KIND_CHAINED ? s.fe : 0;
     }
     return (int)segs.size();
 }

@@ -45,13 +45,14 @@ __global__ void __launch_bounds__(kBlock) hm_tile_plan_kernel(const PlanArgs A) 
 
 __global__ void __launch_bounds__(kBlock) hm_kw_table_kernel(uint32_t* __restrict__ out,
                                                              uint32_t f, uint32_t n,
+                                                             uint64_t base,
                                                              uint64_t total_bits) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    // f digits of t with leading zeros (t < 10^f), then 0x80 and the length
+    // f digits of base + t with leading zeros (< 10^f), then 0x80 and the length
     uint32_t b[32];
     const uint32_t zero[16] = {0};
-    build_tail(b, zero, 0, f, 0, t, 1, total_bits);
+    build_tail(b, zero, 0, f, 0, base + t, 1, total_bits);
     uint32_t w[64];
 #pragma unroll
     for (int k = 0; k < 64; ++k) w[k] = k < 16 ? b[k] : 0u;
@@ -122,12 +123,14 @@ hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipS
     return hipGetLastError();
 }
 
-hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s) {
-    if (f < 1 || f > kMaxChainedF) return hipErrorInvalidValue;
+hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base,
+                           uint64_t total_bits, hipStream_t s) {
+    // the final block holds f digits, 0x80 and the 8-byte length: f <= 55
+    if (fe < 1 || fe > kMaxTableDigits || fe > f || f > 20) return hipErrorInvalidValue;
     uint32_t n = 1;
-    for (uint32_t i = 0; i < f; ++i) n *= 10u;
+    for (uint32_t i = 0; i < fe; ++i) n *= 10u;
     hipLaunchKernelGGL(hm_kw_table_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                       out, f, n, total_bits);
+                       out, f, n, base, total_bits);
     return hipGetLastError();
 }
 

@@ -64,21 +64,26 @@ struct TiledArgs {
     uint32_t s0_loop[100];    // sigma0 of the loop-digit part of W[W1], index t1*10+t0
 };
 
-// Chained scan (two-block tails whose final block holds only 1..4 digits):
-// lanes vary the last q <= 5 digits of tail block 0 (W15, W14's last byte), the final
-// block's digits are the loop index t and its schedule comes from a table of
-// K[i]+W[i] (kMaxChainedTable entries x 64 words).
+// Chained scan (two-block tails): lanes vary the last q <= 5 digits of tail
+// block 0 (W15, W14's last byte), the final block's digits are the loop index
+// t and its schedule comes from a table of K[i]+W[i] per loop value.  A final
+// block of f <= kMaxChainedF digits has one table of 10^f rows.  With more
+// final-block digits (f >= 5) the table covers the low fe = min(f,
+// kMaxTableDigits) of them and the high f - fe digits form an *epoch*: one
+// table and one set of launches per epoch (ChainedArgs::ebase).
 constexpr uint32_t kMaxChainedF = 4;
-constexpr uint32_t kMaxChainedTable = 10000;
+constexpr uint32_t kMaxTableDigits = 7;      // table rows <= 10^7 (2.56 GB)
+constexpr uint32_t kMaxChainedTable = 10000; // rows allocated at hm_open (grown on demand)
 struct ChainedArgs {
     const uint32_t* rec;     // tile records (state = midstate, W = tail block 0)
-    const uint32_t* kwt;     // [10^f][64] K+W of the final block per loop value
+    const uint32_t* kwt;     // [nloop][64] K+W of the final block per loop value
     unsigned int* counter;
     uint64_t* cand;
     uint64_t* sums;          // checked scans only (see TiledArgs)
     uint64_t tile0;
     uint64_t pow10qf;        // nonces per tile = 10^(q+f)
-    uint64_t pow10f;         // loop values = 10^f
+    uint64_t pow10f;         // nonces per lane value = 10^f (f final-block digits)
+    uint64_t ebase;          // epoch e * nloop: the final block's high f - fe digits
     uint64_t seg_lo, seg_hi;
     uint32_t ntasks;         // task ids: nbig whole units, then kSplit per remaining unit
     uint32_t nbig;           // units (lane chunk x loop chunk) dequeued whole
@@ -87,6 +92,7 @@ struct ChainedArgs {
     uint32_t tch;            // loop values per loop chunk
     uint32_t vmax;           // 10^q - 1
     uint32_t q;              // lane digits (<= 5: W15 and the last byte of W14)
+    uint32_t nloop;          // loop values per lane value and epoch = table rows = 10^fe
 };
 
 // Generic scan: one nonce per lane (small / irregular segments, cross-checks).
@@ -110,7 +116,9 @@ hipError_t launch_tile_plan(const PlanArgs& a, hipStream_t s);
 // acc[0] += sum of sums[2i], acc[1] += sum of sums[2i+1] for i < n (wrapping).
 hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipStream_t s);
 // K+W table of the final block for loop values t in [0, 10^f).
-hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint64_t total_bits, hipStream_t s);
+// rows t < 10^fe of the final block holding the f digits of base + t
+hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base,
+                           uint64_t total_bits, hipStream_t s);
 // Fold n (key, nonce) pairs (pair i at cand + 2*i*stride) plus *best into
 // *best (lexicographic min).
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,

@@ -49,7 +49,53 @@ MsgPlan plan_message(const uint8_t* msg, uint64_t len) {
     return mp;
 }
 
-static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
+static void tiled_layout(const MsgPlan& mp, SegPlan& s);
+
+// Final-block digits a chained K+W table covers (10^7 rows, 2.56 GB: with 3
+// lane digits a launch then covers 10^10 nonces, ~0.2 s, so its tail is
+// small); more final-block digits run as epochs (kernels.hpp kMaxTableDigits).
+constexpr uint32_t kTableDigits = 7;
+// Loop values per unit of a chained layout with >= 5 final-block digits:
+// 64 lanes x 100 table-driven blocks, a wave's task ~1 ms (block 0 adds 1 %).
+constexpr uint32_t kEpochTch = 100;
+
+double chained_lane_eff(const SegPlan& s) {
+    const uint64_t P = s.pow10V, S = pow10_u64(s.f);
+    const uint64_t tlo = s.lo / P, thi = s.hi / P;
+    const uint64_t cf = (s.lo - tlo * P) / S / 64, cl = (s.hi - thi * P) / S / 64;
+    const long double chunks = (long double)(thi - tlo) * s.tpt + (long double)cl - (long double)cf + 1;
+    return (double)(((long double)(s.hi - s.lo) + 1) / (chunks * 64.0L * (long double)S));
+}
+
+// Two-block tails with f >= 5 final-block digits whose tail block 0 holds
+// >= 3 digits: the chained layout (lanes in block 0, the final block from a
+// K+W table, epochs beyond 10^7 rows) replaces the tiled one when its
+// modelled cost, with the out-of-range lanes of its edge chunks, is lower.
+static void consider_chained_epochs(const MsgPlan& mp, SegPlan& s, int table_digits) {
+    const uint32_t f = s.T - 64;
+    if (table_digits < 0) return;
+    const uint32_t q = std::min<uint32_t>(5u, 64u - mp.r);  // 64 - r digits in block 0
+    if (f < 5 || q < 3 || q + f > 19) return;  // 10^(q+f) nonces per tile fit in u64
+    SegPlan c = s;  // W1 / straddle keep the tail's geometry, as for f <= 4
+    c.kind = HM_KIND_CHAINED;
+    c.trailer = false;
+    c.lane3 = false;
+    c.lane_shift = c.loop_shift = 0;
+    c.f = f;
+    c.fe = std::min(f, table_digits >= 1 && table_digits <= (int)kTableDigits ? (uint32_t)table_digits
+                                                                                 : kTableDigits);
+    c.q = q;
+    c.V = q + f;
+    c.pow10V = pow10_u64(c.V);
+    c.tpt = (uint32_t)((pow10_u64(q) + 63) / 64);
+    c.tch = (uint32_t)std::min<uint64_t>(kEpochTch, pow10_u64(c.fe));
+    c.ntc = (uint32_t)(pow10_u64(c.fe) / c.tch);
+    c.tile_lo = c.lo / c.pow10V;
+    c.tile_hi = c.hi / c.pow10V;
+    if (seg_cost(c) < seg_cost(s)) s = c;
+}
+
+static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic, int table_digits) {
     s.T = mp.r + s.d;
     s.nb = (s.T + 9 <= 64) ? 1 : 2;
     s.fb = (s.T - 1) / 64;
@@ -62,7 +108,7 @@ static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
     s.trailer = (s.nb - 1 > s.fb);
     s.V = s.q = s.lane_shift = s.loop_shift = s.tpt = 0;
     s.lane3 = false;
-    s.f = s.tch = s.ntc = 0;
+    s.f = s.fe = s.tch = s.ntc = 0;
     s.pow10V = 1;
     s.tile_lo = s.tile_hi = 0;
     if (force_generic) return;
@@ -76,6 +122,7 @@ static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
         if (q >= 2) {
             s.kind = HM_KIND_CHAINED;
             s.f = f;
+            s.fe = f;
             s.q = q;
             s.V = q + f;
             s.pow10V = pow10_u64(s.V);
@@ -88,6 +135,13 @@ static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
             return;
         }
     }
+    tiled_layout(mp, s);
+    if (s.fb == 1) consider_chained_epochs(mp, s, table_digits);
+}
+
+// The tiled layout of segment s, if any (else s stays generic).
+static void tiled_layout(const MsgPlan& mp, SegPlan& s) {
+    const uint32_t k = s.p_end % 4;
     if (s.W1 < 1) return;
     const uint32_t ds = (s.fb == 0) ? mp.r : 0;  // first digit byte within block fb
     const uint32_t vs = std::max<uint32_t>(4u * (uint32_t)(s.W1 - 1), ds);
@@ -117,7 +171,8 @@ static void layout(const MsgPlan& mp, SegPlan& s, bool force_generic) {
     s.kind = HM_KIND_TILED;
 }
 
-std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic) {
+std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic,
+                                int table_digits) {
     std::vector<SegPlan> out;
     const uint32_t d0 = digits_u64(lo), d1 = digits_u64(hi);
     for (uint32_t d = d0; d <= d1; ++d) {
@@ -128,7 +183,7 @@ std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, boo
         s.lo = std::max(lo, dlo);
         s.hi = std::min(hi, dhi);
         if (s.lo > s.hi) continue;
-        layout(mp, s, force_generic);
+        layout(mp, s, force_generic, table_digits);
         out.push_back(s);
     }
     return out;
@@ -146,7 +201,10 @@ double seg_cost(const SegPlan& s) {
             if (s.trailer) return 6980.0;  // digit block + constant trailer block (W1 13..15)
             return kTiled[std::min(std::max(s.W1, 1), 13)];
         case HM_KIND_CHAINED:
-            // per-lane block 0 amortised over 10^f table-driven final blocks
+            // per-lane block 0 amortised over 10^f table-driven final blocks;
+            // f >= 5: block 0 once per 100 loop values (+1 %), and the edge
+            // chunks' out-of-range lanes
+            if (s.f >= 5) return 3275.0 / chained_lane_eff(s);
             return s.f == 1 ? 3777.0 : 3240.0;
         default:
             // generic: every tail block per lane, no hoisting (estimate)

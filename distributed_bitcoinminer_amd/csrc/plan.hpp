@@ -36,8 +36,9 @@ struct SegPlan {
     uint32_t lane_shift, loop_shift;
     uint64_t pow10V;
     uint32_t tpt;               // lane chunks (waves) per tile
-    // chained layout (kind HM_KIND_CHAINED): f digits in the final block
-    uint32_t f, tch, ntc;       // final-block digits; loop values per task; loop chunks
+    // chained layout (kind HM_KIND_CHAINED): f digits in the final block, the
+    // low fe of them from a K+W table of 10^fe rows, the high f - fe as epochs
+    uint32_t f, fe, tch, ntc;   // final-block digits; table digits; loop values per unit; loop chunks
     uint64_t tile_lo, tile_hi;  // inclusive tile range
     uint64_t total_bits;
 };
@@ -45,8 +46,16 @@ struct SegPlan {
 uint32_t digits_u64(uint64_t n);
 uint64_t pow10_u64(uint32_t k);  // k <= 19
 MsgPlan plan_message(const uint8_t* msg, uint64_t len);
-// Segment list for inclusive [lo, hi] (lo <= hi).
-std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic);
+// Segment list for inclusive [lo, hi] (lo <= hi).  table_digits (1..6, 0 =
+// default 6) caps the final-block digits a chained K+W table covers; -1 turns
+// the chained layout of >= 5 final-block digits off (HM_OPT_TABLE_DIGITS, a
+// test hook: small tables make epochs on small ranges).
+std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic,
+                                int table_digits = 0);
+// Fraction of the nonces a chained layout hashes that lie in [s.lo, s.hi]: its
+// lanes vary block-0 digits (nonce stride 10^f), so the 64-lane chunks at the
+// range's two ends carry out-of-range lane values.
+double chained_lane_eff(const SegPlan& s);
 // Modelled GPU cost of one nonce of segment s: SIMD cycles per 64 nonces of
 // the kernel instantiation that runs it, as measured per layout on MI355X
 // (DESIGN.md §4 "Every layout").  Only shard balancing uses it.

@@ -205,6 +205,8 @@ __global__ void HM_TILED_BOUNDS hm_tiled_csum_kernel(const TiledArgs A) {
 // ---------------------------------------------------------------------------
 // Chained scan: per lane one compression of tail block 0 per task, then one
 // table-driven compression per loop value (the final block is wave-uniform).
+// With an epoch (f > fe final-block digits) the loop covers the low fe digits
+// and A.ebase supplies the high ones.
 // ---------------------------------------------------------------------------
 template <bool CSUM>
 DEV void chained_body(const ChainedArgs& A) {
@@ -262,11 +264,11 @@ DEV void chained_body(const ChainedArgs& A) {
         // chaining value into the final block (per lane)
         const State cs{s.a + st[0], s.b + st[1], s.c + st[2], s.d + st[3],
                        s.e + st[4], s.f + st[5], s.g + st[6], s.h + st[7]};
-        const uint64_t nbase = (A.tile0 + tile) * A.pow10qf + (uint64_t)v * A.pow10f;
+        const uint64_t nbase = (A.tile0 + tile) * A.pow10qf + (uint64_t)v * A.pow10f + A.ebase;
         const uint32_t piece = (A.tch + nparts - 1) / nparts;
         const uint32_t t_begin = tc * A.tch + part * piece;
         uint32_t t_end = tc * A.tch + A.tch;
-        if (t_end > (uint32_t)A.pow10f) t_end = (uint32_t)A.pow10f;
+        if (t_end > A.nloop) t_end = A.nloop;
         if (t_end > t_begin + piece) t_end = t_begin + piece;
         const_u32* kw = (const_u32*)(A.kwt + (size_t)t_begin * 64);
         for (uint32_t t = t_begin; t < t_end; ++t, kw += 64) {

@@ -130,6 +130,13 @@ typedef struct hm_stats {
                                   segments on a high-priority stream, the
                                   others on low-priority streams that fill
                                   its last launch's tail; 1 = strictly serial */
+#define HM_OPT_TABLE_DIGITS 7  /* test hook (-1..7, 0 = default 7): the final-
+                                  block digits one K+W table of the chained
+                                  kernel covers; the remaining high final-block
+                                  digits run as epochs (one table each).  Smaller
+                                  values exercise the epochs on small ranges;
+                                  -1 keeps final blocks of >= 5 digits on the
+                                  tiled kernel (ABI 1.5)                        */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */

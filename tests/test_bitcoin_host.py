@@ -117,12 +117,34 @@ def test_planner_layouts(L):
             assert (not s["trailer"]) or s["W1"] >= 13
         elif s["kind"] == _lib.HM_KIND_CHAINED:
             f = T - 64                              # digits in the final block
-            assert fb == 1 and 1 <= f <= 4
             q = s["V"] - f                          # lane digits, W15 (+ W14's last byte) of block 0
-            assert 2 <= q <= 5 and q == min(5, 64 - r)
+            assert fb == 1 and s["f"] == f and q == min(5, 64 - r)
+            if f <= 4:                              # one table of 10^f rows
+                assert 2 <= q <= 5 and s["fe"] == f
+            else:                                   # table of the low fe digits, epochs above
+                assert 3 <= q <= 5 and q + f <= 19 and s["fe"] == min(f, 7) and s["tch"] == 100
         else:
             assert s["kind"] == _lib.HM_KIND_GENERIC
     assert prev_hi == MAX
+
+
+def test_planner_chained_epochs_where_cheaper():
+    """Two-block tails with >= 5 final-block digits go chained (lanes in block
+    0, K+W table of the low fe <= 6 final digits, epochs above) when the
+    range spans enough lane values; a narrow range keeps the tiled layout,
+    whose lanes vary the low digits."""
+    m60 = b"x" * 60                                  # r = 61: 3 digits in block 0
+    seg = _lib.debug_plan(m60, 10**9, 10**10 - 1)[0]  # d = 10: f = 7
+    assert seg["kind"] == _lib.HM_KIND_CHAINED and (seg["f"], seg["fe"]) == (7, 7)
+    narrow = _lib.debug_plan(m60, 5 * 10**9, 5 * 10**9 + 10**8)[0]
+    assert narrow["kind"] == _lib.HM_KIND_TILED and narrow["W1"] == 1
+    m58 = b"y" * 58                                  # r = 59: 5 digits in block 0
+    seg = _lib.debug_plan(m58, 10**9, 10**10 - 1)[0]  # f = 5: one table, no epochs
+    assert seg["kind"] == _lib.HM_KIND_CHAINED and (seg["f"], seg["fe"]) == (5, 5)
+    assert seg["cost"] < 3300
+    # cfg3's 120-B message keeps its f <= 4 tables (d = 8..10)
+    assert all(s["kind"] == _lib.HM_KIND_CHAINED and s["f"] == s["fe"] <= 3
+               for s in _lib.debug_plan(bytes(120), 10**7, 2**32 - 1))
 
 
 def test_planner_bradfitz_2p32():

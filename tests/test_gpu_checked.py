@@ -156,12 +156,23 @@ def test_checked_full_size_pinned(ctx, case):
 
 
 def test_checked_beyond_cpu(ctx):
-    """1.2e11 nonces at d=12 as two chunked launches of 2^20 tiles (a 56-B
-    message: two-block tail, W1 = 1, 10^5-nonce tiles), and 1.2e11 nonces of
-    bradfitz at d=12 (three-word lanes, one launch): no CPU can rescan them,
-    so the counts must be exact, shards split at the launch boundary and
-    elsewhere must add up, and windows must match the generic kernel."""
+    """1.2e11 nonces at d=12 of a 56-B message (two-block tail with 5
+    final-block digits: the chained kernel with a 10^5-row table since round
+    3; the tiled kernel as two chunked launches of 2^20 tiles of 10^5 nonces
+    when the chained layout is switched off -- both must give the same min,
+    key sum and count), and 1.2e11 nonces of bradfitz at d=12 (three-word
+    lanes, one launch): no CPU can rescan them, so the counts must be exact,
+    shards split at the launch boundary and elsewhere must add up, and
+    windows must match the generic kernel."""
     lo, hi = 10**11, 10**11 + 120_000_000_000
+    ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, -1)
+    try:
+        tiled = ctx.scan_checked(b"x" * 56, lo, hi)
+        assert ctx.stats()["dom_kernel"].startswith("hm_tiled_csum_kernel<1, ")
+    finally:
+        ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
+    assert ctx.scan_checked(b"x" * 56, lo, hi) == tiled
+    assert ctx.stats()["dom_kernel"] == "hm_chained_csum_kernel"
     for m in (b"x" * 56, b"bradfitz"):
         whole = ctx.scan_checked(m, lo, hi)
         assert whole[2] == hi - lo + 1

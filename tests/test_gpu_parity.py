@@ -349,13 +349,26 @@ def test_chunked_tile_launches(ctx):
     block 1 (W1 = 1, no room for three-word lanes): V=5, 10^5-nonce tiles, so
     1.2e11 nonces = 1.2 M tiles -> 2 launches.  Checked by shard invariance
     across the launch boundary and the generic kernel on a window around it."""
-    from distributed_bitcoinminer_amd.parallel import merge
     m = b"x" * 56
     lo, hi = 10**11, 10**11 + 120_000_000_000
-    seg = _lib.debug_plan(m, lo, hi)[0]
-    assert seg["kind"] == _lib.HM_KIND_TILED and seg["V"] == 5 and seg["W1"] == 1
+    # the planner runs this layout chained (round 3, f = 5 final-block
+    # digits) unless told otherwise; the two kernels must agree on all 1.2e11
+    assert _lib.debug_plan(m, lo, hi)[0]["kind"] == _lib.HM_KIND_CHAINED
+    ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, -1)
+    try:
+        tiled = _chunked_tiled(ctx, m, lo, hi)
+    finally:
+        ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
+    assert ctx.scan(m, lo, hi) == tiled
+    assert ctx.stats()["dom_kernel"] == "hm_chained_kernel"
+
+
+def _chunked_tiled(ctx, m, lo, hi):
+    from distributed_bitcoinminer_amd.parallel import merge
     whole = ctx.scan(m, lo, hi)
-    assert ctx.stats()["dom_launches"] >= 2
+    st = ctx.stats()
+    assert st["dom_kernel"].startswith("hm_tiled_kernel<1, "), st
+    assert st["dom_launches"] >= 2
     boundary = (lo // 10**5 + (1 << 20)) * 10**5  # first nonce of the 2nd launch
     parts = [ctx.scan(m, lo, boundary - 7), ctx.scan(m, boundary - 6, hi)]
     assert merge(parts) == whole
@@ -367,3 +380,4 @@ def test_chunked_tile_launches(ctx):
     finally:
         ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
     assert _lib.host_hash(m, whole[1]) == whole[0]
+    return whole
