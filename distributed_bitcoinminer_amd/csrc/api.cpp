@@ -335,25 +335,39 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
 // table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of >= 5 digits); the
 // old table may still be read by work queued earlier on any stream, so the
 // device's streams are drained first.
+// Returns HM_ERR_NOMEM (with HIP's error state cleared) when the device
+// cannot hold the table; the caller then plans smaller tables.
 int kw_table_rows(Device& dv, int si, uint64_t rows) {
     if (rows <= dv.kwt_rows[si]) return HM_OK;
     for (int q = 0; q < kStreams; ++q) HIPCHK(hipStreamSynchronize(dv.stream[q]));
-    HIPCHK(hipFree(dv.kwt[si]));
+    if (dv.kwt[si]) HIPCHK(hipFree(dv.kwt[si]));
     dv.kwt[si] = nullptr;
     dv.kwt_rows[si] = 0;
-    HIPCHK(hipMalloc(&dv.kwt[si], (size_t)rows * 64 * sizeof(uint32_t)));
+    if (hipMalloc(&dv.kwt[si], (size_t)rows * 64 * sizeof(uint32_t)) != hipSuccess) {
+        (void)hipGetLastError();
+        dv.kwt[si] = nullptr;
+        return HM_ERR_NOMEM;
+    }
     dv.kwt_rows[si] = rows;
     return HM_OK;
 }
 
-int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si,
+int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& plan, int si,
                     uint64_t* best) {
     hipStream_t st = dv.stream[si];
-    if (s.fe < 1 || s.fe > kMaxTableDigits || s.fe > s.f) return HM_ERR_INTERNAL;
+    if (plan.fe < 1 || plan.fe > kMaxTableDigits || plan.fe > plan.f) return HM_ERR_INTERNAL;
+    // a device short of memory for the planned table gets smaller tables and
+    // more epochs: the same nonces on the same kernel, more launches
+    SegPlan s = plan;
+    int rc;
+    while ((rc = kw_table_rows(dv, si, pow10_u64(s.fe))) == HM_ERR_NOMEM && s.fe > 1) {
+        --s.fe;
+        s.tch = (uint32_t)std::min<uint64_t>(s.tch, pow10_u64(s.fe));
+        s.ntc = (uint32_t)(pow10_u64(s.fe) / s.tch);
+    }
+    if (rc) return rc;
     const uint64_t nloop = pow10_u64(s.fe);       // table rows = loop values per lane
     const uint64_t nep = pow10_u64(s.f - s.fe);   // epochs: the final block's high digits
-    int rc = kw_table_rows(dv, si, nloop);
-    if (rc) return rc;
     const uint64_t per_tile = (uint64_t)s.tpt * s.ntc;
     const uint64_t max_tiles = std::min<uint64_t>(kMaxTilesPerLaunch, 0x7fffffffull / per_tile);
     for (uint64_t e = 0; e < nep; ++e) {
