@@ -352,9 +352,86 @@ int kw_table_rows(Device& dv, int si, uint64_t rows) {
     return HM_OK;
 }
 
+// One chained launch: tiles [t, t + nt) of segment s in epoch e (final-block
+// values e * nloop + [0, nloop), K+W table already built on stream si).
+int launch_chained_tiles(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s, int si,
+                         uint64_t* best, uint64_t t, uint64_t nt, uint64_t e, uint64_t nep) {
+    hipStream_t st = dv.stream[si];
+    const uint64_t nloop = pow10_u64(s.fe);
+    PlanArgs pa;
+    pa.rec = dv.rec[si];
+    pa.tile0 = t;
+    pa.pow10V = s.pow10V;
+    pa.total_bits = s.total_bits;
+    pa.ntiles = (uint32_t)nt;
+    pa.V = s.V;
+    pa.d = s.d;
+    pa.r = mp.r;
+    pa.fb = 0;  // keep tail block 0 raw; its compression is per lane
+    pa.nb = s.nb;
+    memcpy(pa.pw, mp.pw, sizeof pa.pw);
+    memcpy(pa.mid, mp.mid, sizeof pa.mid);
+    HIPCHK(launch_tile_plan(pa, st));
+    ChainedArgs ca;
+    ca.rec = dv.rec[si];
+    ca.kwt = dv.kwt[si];
+    ca.counter = dv.counter[si];
+    ca.cand = dv.cand[si];
+    ca.sums = ctx->csum ? dv.sums[si] : nullptr;
+    ca.tile0 = t;
+    ca.pow10qf = s.pow10V;
+    ca.pow10f = pow10_u64(s.f);
+    ca.ebase = e * nloop;
+    ca.nloop = (uint32_t)nloop;
+    ca.seg_lo = s.lo;
+    ca.seg_hi = s.hi;
+    uint32_t unit0;
+    uint64_t nunits;
+    launch_units(s, t, nt, s.ntc, pow10_u64(s.f), &unit0, &nunits);
+    ca.tpt = s.tpt;
+    ca.ntc = s.ntc;
+    ca.tch = s.tch;
+    ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
+    ca.q = s.q;
+    const Device::Fn* fn = nullptr;
+    int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
+    if (rc) return rc;
+    const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ca.ntasks, &ca.nbig);
+    // every task compresses its lanes' tail block 0 once; the final block
+    // runs once per lane and loop value: nunits * tch values per lane
+    const double block0_per_value = (double)ca.ntasks / ((double)nunits * (double)s.tch);
+    // task ids start at unit0 (the queue counter too): the kernels map a
+    // task below nbig to that unit, so the skipped units are never dequeued
+    ca.ntasks += unit0;
+    ca.nbig += unit0;
+    HIPCHK(hipMemsetD32Async((hipDeviceptr_t)dv.counter[si], (int)unit0, 1, st));
+    Launch L;
+    rc = next_event(dv, &L.start);
+    if (rc) return rc;
+    rc = next_event(dv, &L.stop);
+    if (rc) return rc;
+    // the epochs split every lane value's nonces evenly (stats only)
+    const uint64_t span = tile_span_nonces(s, t, nt);
+    L.nonces = span / nep + (e + 1 == nep ? span % nep : 0);
+    L.kind = HM_KIND_CHAINED;
+    snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
+    L.grid = grid;
+    L.compressions = count_compressions(s);
+    L.comp_eff = 1.0 + block0_per_value;
+    HIPCHK(hipEventRecord(L.start, st));
+    rc = launch_scan(*fn, ca, grid, st);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(L.stop, st));
+    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si, st));
+    if (ctx->csum)
+        HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize),
+                               dv.acc + 2 * si, st));
+    dv.launches.push_back(L);
+    return HM_OK;
+}
+
 int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& plan, int si,
                     uint64_t* best) {
-    hipStream_t st = dv.stream[si];
     if (plan.fe < 1 || plan.fe > kMaxTableDigits || plan.fe > plan.f) return HM_ERR_INTERNAL;
     // a device short of memory for the planned table gets smaller tables and
     // more epochs: the same nonces on the same kernel, more launches
@@ -371,82 +448,14 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& p
     const uint64_t per_tile = (uint64_t)s.tpt * s.ntc;
     const uint64_t max_tiles = std::min<uint64_t>(kMaxTilesPerLaunch, 0x7fffffffull / per_tile);
     for (uint64_t e = 0; e < nep; ++e) {
-      HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.fe, e * nloop, s.total_bits, st));
-      for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
-        const uint64_t nt = std::min<uint64_t>(max_tiles, s.tile_hi - t + 1);
-        PlanArgs pa;
-        pa.rec = dv.rec[si];
-        pa.tile0 = t;
-        pa.pow10V = s.pow10V;
-        pa.total_bits = s.total_bits;
-        pa.ntiles = (uint32_t)nt;
-        pa.V = s.V;
-        pa.d = s.d;
-        pa.r = mp.r;
-        pa.fb = 0;  // keep tail block 0 raw; its compression is per lane
-        pa.nb = s.nb;
-        memcpy(pa.pw, mp.pw, sizeof pa.pw);
-        memcpy(pa.mid, mp.mid, sizeof pa.mid);
-        HIPCHK(launch_tile_plan(pa, st));
-        ChainedArgs ca;
-        ca.rec = dv.rec[si];
-        ca.kwt = dv.kwt[si];
-        ca.counter = dv.counter[si];
-        ca.cand = dv.cand[si];
-        ca.sums = ctx->csum ? dv.sums[si] : nullptr;
-        ca.tile0 = t;
-        ca.pow10qf = s.pow10V;
-        ca.pow10f = pow10_u64(s.f);
-        ca.ebase = e * nloop;
-        ca.nloop = (uint32_t)nloop;
-        ca.seg_lo = s.lo;
-        ca.seg_hi = s.hi;
-        uint32_t unit0;
-        uint64_t nunits;
-        launch_units(s, t, nt, s.ntc, pow10_u64(s.f), &unit0, &nunits);
-        ca.tpt = s.tpt;
-        ca.ntc = s.ntc;
-        ca.tch = s.tch;
-        ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
-        ca.q = s.q;
-        const Device::Fn* fn = nullptr;
-        rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
-        if (rc) return rc;
-        const int grid = plan_launch(ctx, dv, fn->blocks_per_cu, nunits, &ca.ntasks, &ca.nbig);
-        // every task compresses its lanes' tail block 0 once; the final block
-        // runs once per lane and loop value: nunits * tch values per lane
-        const double block0_per_value = (double)ca.ntasks / ((double)nunits * (double)s.tch);
-        // task ids start at unit0 (the queue counter too): the kernels map a
-        // task below nbig to that unit, so the skipped units are never dequeued
-        ca.ntasks += unit0;
-        ca.nbig += unit0;
-        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)dv.counter[si], (int)unit0, 1, st));
-        Launch L;
-        rc = next_event(dv, &L.start);
-        if (rc) return rc;
-        rc = next_event(dv, &L.stop);
-        if (rc) return rc;
-        // the epochs split every lane value's nonces evenly (stats only)
-        const uint64_t span = tile_span_nonces(s, t, nt);
-        L.nonces = span / nep + (e + 1 == nep ? span % nep : 0);
-        L.kind = HM_KIND_CHAINED;
-        snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_chained_csum_kernel" : "hm_chained_kernel");
-        L.grid = grid;
-        L.compressions = count_compressions(s);
-        L.comp_eff = 1.0 + block0_per_value;
-        HIPCHK(hipEventRecord(L.start, st));
-        rc = launch_scan(*fn, ca, grid, st);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(L.stop, st));
-        HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best + 2 * si,
-                           st));
-        if (ctx->csum)
-            HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize),
-                                   dv.acc + 2 * si, st));
-        dv.launches.push_back(L);
-        t += nt;
-        if (t == 0) break;
-      }
+        HIPCHK(launch_kw_table(dv.kwt[si], s.f, s.fe, e * nloop, s.total_bits, dv.stream[si]));
+        for (uint64_t t = s.tile_lo; t <= s.tile_hi;) {
+            const uint64_t nt = std::min<uint64_t>(max_tiles, s.tile_hi - t + 1);
+            rc = launch_chained_tiles(ctx, dv, mp, s, si, best, t, nt, e, nep);
+            if (rc) return rc;
+            t += nt;
+            if (t == 0) break;
+        }
     }
     return HM_OK;
 }
