@@ -180,7 +180,7 @@ def fast_scan_sum(msg, lo: int, hi: int, threads: int = 0):
         raise RuntimeError("CPU lacks the SHA extensions (hm_oracle_fast.c)")
     m = _b(msg)
     if threads <= 0:
-        threads = os.cpu_count() or 1
+        threads = min(16, os.cpu_count() or 1)  # the GPU box's per-GPU CPU share
     h, n, s, c = (ctypes.c_uint64() for _ in range(4))
     _load_fast().oracle_fast_scan_sum(m, len(m), lo, hi, threads, ctypes.byref(h), ctypes.byref(n),
                                       ctypes.byref(s), ctypes.byref(c))

@@ -6,7 +6,10 @@ each compared with oracle_scan_sum -- the min (hash, nonce) of the reference
 loop (miner.go:46-59 over hash.go:13-17), the sum of every key mod 2^64 and
 the count.  Messages are 0..200 random bytes (any value), ranges sit around
 random digit-count boundaries or anywhere, from 1 to ~2*10^6 nonces, some
-ending at 2^64-1.  HM_SOAK_SEED picks the sequence; a failure names its case.
+ending at 2^64-1.  One case in five is a two-block tail with 5 final-block
+digits over 1.3-3.2*10^7 nonces (the chained layout with a K+W table, round 3)
+under a random table cap HM_OPT_TABLE_DIGITS (1..5: 10^4..1 epochs).
+HM_SOAK_SEED picks the sequence; a failure names its case.
 Progress goes to stdout every ~10 s (run with -s).
 """
 import os
@@ -16,6 +19,16 @@ import time
 import pytest
 
 MAX = (1 << 64) - 1
+
+
+def _epoch_case(rng):
+    """Lengths whose tail block 0 holds 3..5 digits, f = 5 final-block digits."""
+    L = rng.choice([58, 59, 60, 122, 123, 124])
+    m = bytes(rng.randrange(256) for _ in range(L))
+    d = 5 + 64 - (L + 1) % 64
+    span = rng.randrange(13_000_000, 32_000_000)
+    lo = 10 ** (d - 1) + rng.randrange(0, 9 * 10 ** (d - 1) - span)
+    return m, lo, lo + span - 1, rng.randrange(0, 6)
 
 
 def _case(rng):
@@ -43,11 +56,20 @@ def test_random_soak_checked(ctx, oracle_mod):
     rng = random.Random(seed)
     t0 = last = time.time()
     n = nonces = 0
+    from distributed_bitcoinminer_amd import _lib
     while time.time() - t0 < budget:
-        m, lo, hi = _case(rng)
-        got = ctx.scan_checked(m, lo, hi)
+        table = 0
+        if rng.randrange(5) == 0:
+            m, lo, hi, table = _epoch_case(rng)
+        else:
+            m, lo, hi = _case(rng)
+        ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, table)
+        try:
+            got = ctx.scan_checked(m, lo, hi)
+        finally:
+            ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
         exp = oracle_mod.c_scan_sum(m, lo, hi)
-        assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi)
+        assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi, table)
         n += 1
         nonces += hi - lo + 1
         if time.time() - last > 10:
