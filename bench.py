@@ -143,6 +143,7 @@ OPS_PER_COMPRESSION = 1552
 PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T INT32 lane-ops/s
 CPU_SAMPLE = 50_000_000              # nonces for the 1-thread CPU baseline (~12 s on the GPU box host)
 CPU_FLEET_PER_THREAD = 40_000_000    # nonces per thread of the fleet sample (~9 s)
+CPU_FAST_PER_THREAD = 60_000_000     # nonces per thread of the optimised CPU sample (~5 s)
 
 
 def _cpu_share() -> int:
@@ -176,13 +177,26 @@ def cpu_baseline(msg: bytes, name: str):
     dN = time.perf_counter() - t
     cpu = next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                 if l.startswith("model name")), platform.processor() or "?")
+    # SURVEY §8(d)'s optional "optimised CPU" line: the SHA-extension oracle
+    # (midstate of the constant blocks, digits incremented in place, x86 SHA
+    # instructions), same threads; not the reference's per-nonce work
+    optimised = None
+    if oracle.fast_available():
+        nF = CPU_FAST_PER_THREAD // scale * cores
+        t = time.perf_counter()
+        oracle.fast_scan_sum(msg, 0, nF - 1, threads=cores)
+        dF = time.perf_counter() - t
+        optimised = {"value": nF / dF / 1e9, "unit": "GH/s", "cores": cores,
+                     "sample": f"[0, {nF}) on {cores} threads of oracle/hm_oracle_fast.c "
+                               f"(SHA extensions, midstate, in-place digits), {dF:.2f} s"}
     return {"value": nN / dN / 1e9, "unit": "GH/s", "cores": cores, "kind": "port",
             "sample": f"{name}: a fleet of {cores} CPU miners (one thread each, disjoint equal "
                       f"chunks of [0, {nN})) running oracle/hm_oracle.c, the C restatement of "
                       f"the reference loop (Sprintf-style format + SHA-256 from the IV per "
                       f"nonce, strict <); {dN:.2f} s on {cpu}",
             "single_miner": {"value": n1 / d1 / 1e9, "unit": "GH/s", "cores": 1,
-                             "sample": f"[0, {n1}) on 1 thread, {d1:.2f} s"}}
+                             "sample": f"[0, {n1}) on 1 thread, {d1:.2f} s"},
+            "optimised": optimised}
 
 
 ROUND_OPS = 16      # lane-ops per SHA-256 round
