@@ -136,7 +136,7 @@ hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipS
 
 hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base,
                            uint64_t total_bits, hipStream_t s) {
-    // the final block holds f digits, 0x80 and the 8-byte length: f <= 55
+    // f final-block digits (a u64 has at most 20), fe of them from the table
     if (fe < 1 || fe > kMaxTableDigits || fe > f || f > 20) return hipErrorInvalidValue;
     uint32_t n = 1;
     for (uint32_t i = 0; i < fe; ++i) n *= 10u;

@@ -110,3 +110,18 @@ def test_default_tables_config_size(ctx, oracle_mod, table_digits):
     table_digits(6)
     _check(ctx, oracle_mod, m, lo, hi)
     assert ctx.stats()["dom_launches"] == 10
+
+
+def test_top_of_the_nonce_space(ctx, oracle_mod, table_digits):
+    """20-digit nonces up to 2^64-1 (len 48: 15 digits in block 0, f = 5): the
+    last tile is cut by 2^64-1, so lanes and epochs past it compute wrapped
+    nonces that the range mask must drop.  One table, 10^2 and 10^1 rows."""
+    MAX = (1 << 64) - 1
+    m = bytes(random.Random(48).randrange(33, 127) for _ in range(48))
+    for lo, hi in ((MAX - 30_000_000, MAX), (MAX - 25_123_457, MAX - 1_234_567)):
+        exp = oracle_mod.fast_scan_sum(m, lo, hi, threads=THREADS)
+        for k in (0, 2, 1):
+            table_digits(k)
+            seg = _lib.debug_plan(m, lo, hi)[0]
+            assert seg["kind"] == _lib.HM_KIND_CHAINED and seg["f"] == 5
+            assert ctx.scan_checked(m, lo, hi) == exp, (lo, hi, k)
