@@ -163,3 +163,40 @@ def test_planner_empty_and_single():
     assert _lib.debug_plan(b"x", 5, 4) == []
     s = _lib.debug_plan(b"x", MAX, MAX)
     assert len(s) == 1 and s[0]["lo"] == s[0]["hi"] == MAX
+
+
+def test_planner_chained_epoch_cost_model():
+    """The f >= 5 chained layout's modelled cost is 3275 SIMD cycles per 64
+    nonces over the fraction of hashed nonces inside [lo, hi] (its lanes vary
+    block-0 digits, stride 10^f nonces, so the 64-lane chunks at the range's
+    ends carry out-of-range lanes); it is picked exactly when that beats the
+    tiled layout's cost (plan.cpp consider_chained_epochs)."""
+    import random
+    rng = random.Random(4040)
+    tiled_cost = {s["W1"]: s["cost"] for L in range(0, 45)
+                  for s in _lib.debug_plan(b"x" * L, 10**9, 10**9 + 10**6)
+                  if s["kind"] == _lib.HM_KIND_TILED and not s["trailer"]}
+    n_chained = n_tiled = 0
+    for _ in range(400):
+        L = rng.choice([56, 57, 58, 59, 60, 120, 121, 122, 123, 124])
+        r = (L + 1) % 64
+        q = min(5, 64 - r)
+        d = rng.randrange(64 - r + 5, 20)
+        f = r + d - 64
+        S, P = 10**f, 10**(q + f)
+        span = rng.choice([rng.randrange(1, 64 * S), rng.randrange(64 * S, 64 * S * 40)])
+        span = min(span, (10**d - 10**(d - 1)) // 2)
+        lo = rng.randrange(10**(d - 1), 10**d - span)
+        hi = lo + span - 1
+        seg = _lib.debug_plan(b"x" * L, lo, hi)[0]
+        tpt = -(-10**q // 64)
+        chunks = (hi // P - lo // P) * tpt + (hi % P) // S // 64 - (lo % P) // S // 64 + 1
+        eff = span / (chunks * 64 * S)
+        if seg["kind"] == _lib.HM_KIND_CHAINED:
+            n_chained += 1
+            assert seg["f"] == f and abs(seg["cost"] - int(3275 / eff)) <= 1, (L, lo, hi)
+            assert 3275 / eff < tiled_cost.get(seg["W1"], 6000 * 2)
+        else:
+            n_tiled += 1
+            assert 3275 / eff >= seg["cost"] - 1 or q + f > 19, (L, lo, hi, seg)
+    assert n_chained > 50 and n_tiled > 50, (n_chained, n_tiled)
