@@ -125,3 +125,25 @@ def test_top_of_the_nonce_space(ctx, oracle_mod, table_digits):
             seg = _lib.debug_plan(m, lo, hi)[0]
             assert seg["kind"] == _lib.HM_KIND_CHAINED and seg["f"] == 5
             assert ctx.scan_checked(m, lo, hi) == exp, (lo, hi, k)
+
+
+def test_batches_streams_and_devices(oracle_mod):
+    """Chained f >= 5 segments inside hm_scan_many batches: requests on four
+    streams grow their K+W tables (10^5 and 10^6 rows) while other streams'
+    work is in flight; then the same requests sharded over device 0 opened
+    twice and three times (hm_partition shards, host merge)."""
+    m58 = bytes(random.Random(58).randrange(33, 127) for _ in range(58))
+    m60 = bytes(random.Random(60).randrange(33, 127) for _ in range(60))
+    reqs = [(m58, 10**9 + 4_321_987, 10**9 + 4_321_987 + 31_234_567),     # f = 5, q = 5
+            (m60, 10**7, 10**8 - 1),                                       # f = 5, q = 3
+            (m58, 10**10 + 77_777_777, 10**10 + 77_777_777 + 220_000_000), # f = 6
+            (b"bradfitz", 10**9, 10**9 + 10**7),                           # tiled
+            (m60, 10**7 + 12_345, 10**7 + 12_345)]                         # one nonce
+    assert sum(s["kind"] == _lib.HM_KIND_CHAINED and s["f"] >= 5
+               for m, lo, hi in reqs for s in _lib.debug_plan(m, lo, hi)) >= 3
+    exp = [oracle_mod.fast_scan_sum(m, lo, hi, threads=THREADS)[0] for m, lo, hi in reqs]
+    for devs, streams in (([0], 4), ([0], 1), ([0, 0], 4), ([0, 0, 0], 4)):
+        with _lib.Context(devs) as c:
+            c.set_option(_lib.HM_OPT_STREAMS, streams)
+            assert c.scan_many(reqs) == exp, (devs, streams)
+            assert [c.scan(m, lo, hi) for m, lo, hi in reqs] == exp, (devs, streams)
