@@ -34,6 +34,8 @@ def _free_port():
 
 
 def _torchrun(nproc, args, env_extra, timeout):
+    # generous limits: on a fresh box these children may be the first to
+    # import torch (1-2 minutes while the image pages in)
     env = dict(os.environ, **env_extra)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1",
@@ -48,7 +50,7 @@ def _torchrun(nproc, args, env_extra, timeout):
 
 def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
     line = _torchrun(2, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
-                         "--no-cpu-baseline"], {"HM_BENCH_BACKEND": "gloo"}, timeout=240)
+                         "--no-cpu-baseline"], {"HM_BENCH_BACKEND": "gloo"}, timeout=420)
     assert line["n_gpus"] == 2 and line["config"]["merge"] == "gloo"
     assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
     assert len(line["ranks"]["local_ms"]) == 2
@@ -65,7 +67,7 @@ def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
 
 def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
     line = _torchrun(1, ["--steps", "2", "--warmup", "1", "--secondary", "cfg3",
-                         "--no-cpu-baseline"], {"HM_BENCH_FORCE_DIST": "1"}, timeout=180)
+                         "--no-cpu-baseline"], {"HM_BENCH_FORCE_DIST": "1"}, timeout=300)
     assert line["config"]["merge"] == "RCCL all-gather"
     assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
     c3 = line["workloads"]["cfg3"]
