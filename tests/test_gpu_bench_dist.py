@@ -75,3 +75,21 @@ def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
     rl = c3["roofline"]
     assert rl["kernel"] == "hm_chained_kernel"
     assert 0 < rl["frac_rounds"] < rl["frac"] <= 1.0
+
+
+def test_bench_torchrun_rccl_all_visible_gpus():
+    """With >= 2 visible GPUs (a multi-GPU test box), the driver's launch line
+    itself: one RCCL rank per GPU over xGMI, cfg2 weak ([0, N*2^32)) and the
+    cfg4 strong split of [0, 2^40), both against their oracle fixtures, and
+    every rank reporting its own timing.  Skipped on a 1-GPU box."""
+    import torch
+    n = min(torch.cuda.device_count(), 8)
+    if n < 2:
+        pytest.skip(f"{n} visible GPU(s): the RCCL launch line needs >= 2")
+    line = _torchrun(n, ["--steps", "2", "--warmup", "1", "--secondary", "cfg4",
+                         "--no-cpu-baseline"], {}, timeout=600)
+    assert line["n_gpus"] == n and line["config"]["merge"] == "RCCL all-gather"
+    assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
+    c4 = line["workloads"]["cfg4"]
+    assert c4["result_vs_oracle"]["match"] is True, c4["result_vs_oracle"]
+    assert len(line["ranks"]["local_ms"]) == n and len(c4["ranks"]["local_ms"]) == n
