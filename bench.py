@@ -102,6 +102,52 @@ def fixture_check(msg: bytes, lo: int, hi: int, res):
     return None
 
 
+def _fixture_pieces(msg: bytes):
+    """Every list of contiguous oracle pieces the committed fixtures hold for
+    msg: full_size.json's weak pieces (configs[1]/[2]: [r*2^32, (r+1)*2^32)
+    for r < 8) and its cfg4 pieces (configs[3]: [0, 2^40) in 2^34-nonce
+    pieces, cut at every hm_partition boundary for 1/2/4/8 shards)."""
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+            full = json.load(f)
+    except (OSError, ValueError):
+        return []
+    lists = [w["pieces"] for w in full.get("weak", []) if bytes.fromhex(w["msg_hex"]) == msg]
+    c4 = full.get("cfg4")
+    if c4 and bytes.fromhex(c4["msg_hex"]) == msg:
+        lists.append(c4["pieces"])
+    return lists
+
+
+def shard_check(msg: bytes, lo, hi, res):
+    """One rank's own 16-B answer against the oracle pieces that make up its
+    shard [lo, hi] exactly (None when no fixture covers it).  An empty shard
+    (lo None) must answer the scan's seed (2^64-1, 0)."""
+    if lo is None:
+        return {"fixture": None, "expected": {"hash": MAXU64, "nonce": 0},
+                "match": tuple(res) == (MAXU64, 0)}
+    for pieces in _fixture_pieces(msg):
+        inside = sorted((p for p in pieces if int(p["lo"]) >= lo and int(p["hi"]) <= hi),
+                        key=lambda p: int(p["lo"]))
+        if not inside or int(inside[0]["lo"]) != lo or int(inside[-1]["hi"]) != hi:
+            continue
+        if any(int(b["lo"]) != int(a["hi"]) + 1 for a, b in zip(inside, inside[1:])):
+            continue
+        exp = min((int(p["hash"]), int(p["nonce"])) for p in inside)
+        return {"fixture": "tests/golden/full_size.json",
+                "expected": {"hash": exp[0], "nonce": exp[1]}, "match": tuple(res) == exp}
+    return None
+
+
+def all_match(ranks):
+    """True when every rank's answer equals its fixture piece, False when any
+    differs, None when some rank has no fixture (and none differs)."""
+    m = ranks["match"]
+    if any(x is False for x in m):
+        return False
+    return True if all(x is True for x in m) else None
+
+
 def code_object_sha16():
     """sha256 (16 hex) of the scan kernels' code object embedded in the
     libhipminer.so this process loaded (the bytes hipModuleLoadData gets), so a
@@ -372,6 +418,11 @@ def main():
             dist.init_process_group(backend, rank=rank, world_size=world)
 
     ctx = _lib.Context([gpu])
+    # the library this run measures, and whether it is this tree's build
+    # (hm_build_id vs the digest of csrc/ and include/hipminer.h)
+    from distributed_bitcoinminer_amd import build_id as bid
+    build = {"build_id": _lib.build_id(), "build_matches_tree": _lib.build_id() == bid.tree_digest()}
+    exit_code = 0
     # HM_BENCH_STREAMS=1: strictly serial launches (kernel traces then
     # attribute time without cross-stream queue waits)
     if os.environ.get("HM_BENCH_STREAMS"):
@@ -386,15 +437,22 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(cdev)
 
-    def gather_f64(vals):
-        """All ranks' float64 vectors (one all-gather; the bench's only
-        other collective besides the 16-B candidates)."""
+    def gather(vals, dtype):
+        """All ranks' vectors (one all-gather, outside the timed region; the
+        bench's only collectives besides the 16-B candidates)."""
         if dist is None:
             return [list(vals)]
-        t = torch.tensor(vals, dtype=torch.float64, device=dev)
-        out = torch.empty(world * len(vals), dtype=torch.float64, device=dev)
+        t = torch.tensor(vals, dtype=dtype, device=dev)
+        out = torch.empty(world * len(vals), dtype=dtype, device=dev)
         dist.all_gather_into_tensor(out, t)
         return out.cpu().reshape(world, len(vals)).tolist()
+
+    def gather_f64(vals):
+        return gather(vals, torch.float64)
+
+    # this rank's GPU, reported per rank so a wrong or slow shard names its device
+    props = torch.cuda.get_device_properties(cdev)
+    my_device = [gpu, props.pci_domain_id, props.pci_bus_id, props.pci_device_id]
 
     if dist is not None:
         # communicator set-up (RCCL connects its rings on the first
@@ -404,15 +462,20 @@ def main():
         dist.all_gather_into_tensor(gathered, cand)
         barrier()
 
-    def measure(m, lo, hi, steps, warmup):
+    def measure(m, lo, hi, steps, warmup, shard_bounds):
         """W untimed + K timed steps of (this rank's hm_scan of [lo, hi],
         all-gather of the 16-B candidates, min).  Returns the max-over-ranks
         time, the merged result, rank 0's step times, this rank's hm_stats of
         the last scan and the per-rank timings (each rank's own time to its
         last result, before the closing barrier, and its summed scan-kernel
-        busy time: DVFS or placement imbalance between GPUs shows there)."""
+        busy time: DVFS or placement imbalance between GPUs shows there),
+        with each rank's own answer, device and fixture match (shard_bounds(r)
+        = rank r's inclusive shard, or (None, None) when empty)."""
+        last_local = [None]
+
         def step():
             local = ctx.scan(m, lo, hi) if lo is not None else (MAXU64, 0)
+            last_local[0] = local
             if dist is None:
                 return local
             cand.copy_(torch.from_numpy(np.array(local, dtype=np.uint64).view(np.int64)))
@@ -437,27 +500,49 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         st = ctx.stats() if lo is not None else None
-        per_rank = gather_f64([local_ms, busy_ms, elapsed])
+        kern_ghs = st["dom_nonces"] / (st["dom_kernel_ms"] * 1e-3) / 1e9 \
+            if st and st["dom_kernel_ms"] > 0 else 0.0
+        per_rank = gather_f64([local_ms, busy_ms, elapsed, kern_ghs])
         elapsed = max(r[2] for r in per_rank)
         loc = [round(r[0], 3) for r in per_rank]
+        # per-rank self-check: each rank's own 16-B answer (u64 pair carried
+        # as int64 bits), its device, and its answer against the oracle pieces
+        # of its shard, so a wrong shard names its rank and GPU
+        own = np.array(last_local[0], dtype=np.uint64).view(np.int64).tolist()
+        ids = gather(own + [-1 if lo is None else 0] + my_device, torch.int64)
+        answers, devices, match = [], [], []
+        for r, row in enumerate(ids):
+            a = tuple(int(x) for x in np.array(row[:2], dtype=np.int64).view(np.uint64))
+            answers.append({"hash": a[0], "nonce": a[1]})
+            devices.append({"ordinal": row[3],
+                            "pci_bus_id": f"{row[4]:04x}:{row[5]:02x}:{row[6]:02x}.0"})
+            r_lo, r_hi = shard_bounds(r)
+            chk = shard_check(m, r_lo, r_hi, a)
+            match.append(chk["match"] if chk else None)
         ranks = {"local_ms": loc, "kernel_busy_ms": [round(r[1], 3) for r in per_rank],
                  "local_ms_min": min(loc), "local_ms_max": max(loc),
-                 "spread_pct": round(100.0 * (max(loc) - min(loc)) / max(loc), 3)}
+                 "spread_pct": round(100.0 * (max(loc) - min(loc)) / max(loc), 3),
+                 "kernel_GHs": [round(r[3], 3) for r in per_rank],
+                 "device": devices, "answer": answers, "match": match}
         # self-check: the winner re-hashes to the reported hash (host hm_hash)
         assert _lib.host_hash(m, res[1]) == res[0], res
         return elapsed, res, step_ms, st, ranks
 
-    def shard_of(name):
-        """(total nonces, this rank's inclusive shard or (None, None)).
+    def shard_of(name, r=rank):
+        """(total nonces, rank r's inclusive shard or (None, None)).
         cfg2/cfg3: weak, rank r scans [r*2^32, (r+1)*2^32); cfg4: strong, the
         cost-weighted hm_partition shard of [0, 2^40)."""
         if name == "cfg4":
-            sh = shard_range(0, (1 << 40) - 1, world, rank, msg=WORKLOADS["cfg4"][0])
+            sh = shard_range(0, (1 << 40) - 1, world, r, msg=WORKLOADS["cfg4"][0])
             return 1 << 40, sh if sh is not None else (None, None)
-        return world * PER_GPU, (rank * PER_GPU, (rank + 1) * PER_GPU - 1)
+        return world * PER_GPU, (r * PER_GPU, (r + 1) * PER_GPU - 1)
+
+    def bounds_of(name):
+        return lambda r: shard_of(name, r)[1]
 
     total_nonces, (lo, hi) = shard_of(args.workload)
-    elapsed, res, step_ms, st, ranks = measure(msg, lo, hi, args.steps, args.warmup)
+    elapsed, res, step_ms, st, ranks = measure(msg, lo, hi, args.steps, args.warmup,
+                                               bounds_of(args.workload))
     rl = roofline(st, msg, lo, hi) if rank == 0 else None
 
     # secondaries of the default cfg2 run, so the driver's run also clocks
@@ -473,7 +558,7 @@ def main():
         m2 = long120() if name == "cfg3" else WORKLOADS[name][0]
         tot2, (lo2, hi2) = shard_of(name)
         steps2, warm2 = (max(1, min(args.steps, 5)), 1) if name == "cfg3" else (1, 0)
-        e2, r2, sm2, st2, rk2 = measure(m2, lo2, hi2, steps2, warm2)
+        e2, r2, sm2, st2, rk2 = measure(m2, lo2, hi2, steps2, warm2, bounds_of(name))
         if rank == 0:
             secondary[name] = {
                 "workload": WORKLOADS[name][1], "value": round(tot2 * steps2 / e2 / 1e9, 3),
@@ -485,6 +570,7 @@ def main():
                 "result": {"hash": r2[0], "nonce": r2[1]},
                 "result_vs_oracle": fixture_check(m2, 0, tot2 - 1, r2),
                 "ranks": rk2,
+                "all_ranks_match": all_match(rk2),
                 "roofline": roofline(st2, m2, lo2, hi2) if lo2 is not None else None}
 
     if rank == 0:
@@ -511,6 +597,9 @@ def main():
             "result": {"hash": res[0], "nonce": res[1]},
             "result_vs_oracle": fixture_check(msg, 0, total_nonces - 1, res),
             "ranks": ranks,
+            "all_ranks_match": all_match(ranks),
+            "build_id": build["build_id"],
+            "build_matches_tree": build["build_matches_tree"],
             "roofline": rl,
         }
         if secondary:
@@ -519,9 +608,20 @@ def main():
             cb = cpu_baseline(msg, args.workload)
             line["cpu_baseline"] = cb
         os.write(json_fd, (json.dumps(line) + "\n").encode())
+        # a wrong answer fails the run (after the line is out, so the
+        # mismatching rank and device are on record)
+        checks = [line["result_vs_oracle"], *(w["result_vs_oracle"] for w in secondary.values())]
+        wrong = [c for c in checks if c is not None and c["match"] is False]
+        wrong += [n for n, rk in [("primary", ranks)] + [(k, w["ranks"]) for k, w in secondary.items()]
+                  if all_match(rk) is False]
+        if wrong:
+            print(f"bench: answers differ from the oracle fixtures: {wrong}", file=sys.stderr)
+            exit_code = 1
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+    if exit_code:
+        sys.exit(exit_code)
 
 
 if __name__ == "__main__":

@@ -26,6 +26,7 @@ HM_ERR_INTERNAL = -6
 HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
 HM_OPT_TABLE_DIGITS = 7
+HM_OPT_TABLE_ROWS_CAP = 8
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
@@ -52,7 +53,9 @@ class hm_stats(ctypes.Structure):
                 ("launches", ctypes.c_int32), ("dom_kind", ctypes.c_int32),
                 ("ndev", ctypes.c_int32), ("dom_grid", ctypes.c_int32),
                 ("dom_launches", ctypes.c_int32), ("merge", ctypes.c_int32),
-                ("dom_kernel", ctypes.c_char * 64), ("dom_compressions_eff", ctypes.c_double)]
+                ("dom_kernel", ctypes.c_char * 64), ("dom_compressions_eff", ctypes.c_double),
+                ("enqueue_ms", ctypes.c_double), ("mid_call_syncs", ctypes.c_int32),
+                ("table_grows", ctypes.c_int32)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -110,6 +113,8 @@ def load() -> ctypes.CDLL:
         lib.hm_close.argtypes = [ctypes.c_void_p]
         lib.hm_version.restype = ctypes.c_int
         lib.hm_version.argtypes = []
+        lib.hm_build_id.restype = ctypes.c_char_p
+        lib.hm_build_id.argtypes = []
         lib.hm_partition.restype = ctypes.c_int
         lib.hm_partition.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
@@ -234,6 +239,18 @@ def partition(msg, lo: int, hi: int, n: int) -> list:
         a, b = int(buf[2 * i]), int(buf[2 * i + 1])
         out.append((a, b) if a <= b else None)
     return out
+
+
+def build_id() -> str:
+    """hm_build_id: digest of the sources the loaded library was built from."""
+    return load().hm_build_id().decode()
+
+
+def build_matches_tree() -> bool:
+    """True when the loaded libhipminer.so was built from this tree's sources
+    (build_id.tree_digest over csrc/ and include/hipminer.h)."""
+    from distributed_bitcoinminer_amd import build_id as bid
+    return build_id() == bid.tree_digest()
 
 
 def code_object_sha16() -> str:

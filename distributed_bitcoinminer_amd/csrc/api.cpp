@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/hipminer.h"
+#include "build_id.h"  // generated: HM_BUILD_ID (distributed_bitcoinminer_amd/build_id.py)
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -84,6 +85,7 @@ struct Device {
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
     uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
+    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed after the call
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
@@ -130,6 +132,12 @@ struct hm_ctx {
     int grid_per_cu = 0;
     int streams = kStreams;  // HM_OPT_STREAMS (tail filling by default)
     int table_digits = 0;    // HM_OPT_TABLE_DIGITS (test hook; 0 = default, -1 = off)
+    uint64_t table_rows_cap = 0;  // HM_OPT_TABLE_ROWS_CAP (test hook; 0 = off)
+    // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
+    bool enqueuing = false;
+    int32_t mid_syncs = 0;
+    int32_t table_grows = 0;
+    double enqueue_ms = 0;
     bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
     bool have_stats = false;
     int merge = HM_MERGE_NONE;  // how the current call merged device results
@@ -198,6 +206,8 @@ void device_free(Device& dv) {
         if (s == 0 && dv.t0) (void)hipEventDestroy(dv.t0);
         if (dv.stream[s]) (void)hipStreamDestroy(dv.stream[s]);
     }
+    for (uint32_t* t : dv.retired) (void)hipFree(t);
+    dv.retired.clear();
     for (hipEvent_t e : dv.evpool) (void)hipEventDestroy(e);
     if (dv.mod) (void)hipModuleUnload(dv.mod);
     dv.fns.clear();
@@ -331,25 +341,46 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
+// Host wait for stream st.  Counted in hm_stats.mid_call_syncs when the call
+// is still enqueuing work (on this or a later device): such a wait would hold
+// back every launch after it.
+int host_wait(hm_ctx* ctx, hipStream_t st) {
+    if (ctx->enqueuing) ++ctx->mid_syncs;
+    HIPCHK(hipStreamSynchronize(st));
+    return HM_OK;
+}
+
 // Make stream si's K+W table hold `rows` rows.  Grown once to the largest
-// table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of >= 5 digits); the
-// old table may still be read by work queued earlier on any stream, so the
-// device's streams are drained first.
-// Returns HM_ERR_NOMEM (with HIP's error state cleared) when the device
-// cannot hold the table; the caller then plans smaller tables.
-int kw_table_rows(Device& dv, int si, uint64_t rows) {
+// table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of
+// >= 5 digits).  Work queued earlier on any stream may still read the old
+// table, so it is not freed here (hipFree waits for the device): it is
+// retired and freed after the call's results are read back
+// (release_retired), and the host never blocks mid-enqueue.
+// Returns HM_ERR_NOMEM (with HIP's error state cleared, the old table kept)
+// when the device cannot hold the table, or the HM_OPT_TABLE_ROWS_CAP test
+// hook refuses it; the caller then plans smaller tables.
+int kw_table_rows(hm_ctx* ctx, Device& dv, int si, uint64_t rows) {
     if (rows <= dv.kwt_rows[si]) return HM_OK;
-    for (int q = 0; q < kStreams; ++q) HIPCHK(hipStreamSynchronize(dv.stream[q]));
-    if (dv.kwt[si]) HIPCHK(hipFree(dv.kwt[si]));
-    dv.kwt[si] = nullptr;
-    dv.kwt_rows[si] = 0;
-    if (hipMalloc(&dv.kwt[si], (size_t)rows * 64 * sizeof(uint32_t)) != hipSuccess) {
+    if (ctx->table_rows_cap && rows > ctx->table_rows_cap) return HM_ERR_NOMEM;
+    uint32_t* t = nullptr;
+    if (hipMalloc(&t, (size_t)rows * 64 * sizeof(uint32_t)) != hipSuccess) {
         (void)hipGetLastError();
-        dv.kwt[si] = nullptr;
         return HM_ERR_NOMEM;
     }
+    if (dv.kwt[si]) dv.retired.push_back(dv.kwt[si]);
+    dv.kwt[si] = t;
     dv.kwt_rows[si] = rows;
+    ++ctx->table_grows;
     return HM_OK;
+}
+
+// Free the tables kw_table_rows retired.  Called between calls only (no work
+// of this context in flight), since hipFree synchronises the device.
+void release_retired(Device& dv) {
+    if (dv.retired.empty()) return;
+    (void)hipSetDevice(dv.ordinal);
+    for (uint32_t* t : dv.retired) (void)hipFree(t);
+    dv.retired.clear();
 }
 
 // One chained launch: tiles [t, t + nt) of segment s in epoch e (final-block
@@ -437,7 +468,7 @@ int enqueue_chained(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& p
     // more epochs: the same nonces on the same kernel, more launches
     SegPlan s = plan;
     int rc;
-    while ((rc = kw_table_rows(dv, si, pow10_u64(s.fe))) == HM_ERR_NOMEM && s.fe > 1) {
+    while ((rc = kw_table_rows(ctx, dv, si, pow10_u64(s.fe))) == HM_ERR_NOMEM && s.fe > 1) {
         --s.fe;
         s.tch = (uint32_t)std::min<uint64_t>(s.tch, pow10_u64(s.fe));
         s.ntc = (uint32_t)(pow10_u64(s.fe) / s.tch);
@@ -752,10 +783,16 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
             dr.hi = sh[i].empty ? 0 : sh[i].hi;
         }
     }
+    // every device's work is enqueued before the host waits on any of it
+    const auto te = std::chrono::steady_clock::now();
+    ctx->enqueuing = true;
     for (int i = 0; i < ndev; ++i) {
         int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i], first);
-        if (rc) return rc;
+        if (rc) { ctx->enqueuing = false; return rc; }
     }
+    ctx->enqueuing = false;
+    ctx->enqueue_ms +=
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - te).count();
     if (ctx->merge_rccl) {
         int rc = rccl_merge(ctx, nreq);
         if (rc) return rc;
@@ -766,7 +803,8 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
                               hipMemcpyDeviceToHost, d0.stream[0]));
         for (auto& dv : ctx->devs) {
             HIPCHK(hipSetDevice(dv.ordinal));
-            HIPCHK(hipStreamSynchronize(dv.stream[0]));
+            int rc = host_wait(ctx, dv.stream[0]);
+            if (rc) return rc;
         }
         for (int r = 0; r < nreq; ++r) outs[r] = d0.host_out[r];
         return HM_OK;
@@ -780,7 +818,8 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
     for (int r = 0; r < nreq; ++r) outs[r] = hm_result{~0ull, 0};
     for (auto& dv : ctx->devs) {
         HIPCHK(hipSetDevice(dv.ordinal));
-        HIPCHK(hipStreamSynchronize(dv.stream[0]));
+        int rc = host_wait(ctx, dv.stream[0]);
+        if (rc) return rc;
         for (int r = 0; r < nreq; ++r)
             if (lex_less(dv.host_out[r].hash, dv.host_out[r].nonce, outs[r].hash, outs[r].nonce))
                 outs[r] = dv.host_out[r];
@@ -801,8 +840,14 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
 
 // 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked;
 // 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count;
-// 1.5: hm_scan_stats_sized, HM_OPT_MERGE_RCCL refused up front for repeated ordinals
-int hm_version(void) { return (1 << 16) | 5; }
+// 1.5: hm_scan_stats_sized, HM_OPT_MERGE_RCCL refused up front for repeated ordinals;
+// 1.6: hm_build_id, hm_stats.enqueue_ms / mid_call_syncs / table_grows, HM_OPT_TABLE_ROWS_CAP
+int hm_version(void) { return (1 << 16) | 6; }
+
+// The digest of the sources this library was built from (build_id.py), kept
+// in the binary behind a tag so tools can read it without loading the library.
+static const char kBuildTag[] = "hipminer-build-id:" HM_BUILD_ID;
+const char* hm_build_id(void) { return kBuildTag + sizeof("hipminer-build-id:") - 1; }
 
 int hm_partition(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t* bounds) {
@@ -904,6 +949,10 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
             if (value < -1 || value > (int64_t)kMaxTableDigits) return HM_ERR_INVALID;
             ctx->table_digits = (int)value;
             return HM_OK;
+        case HM_OPT_TABLE_ROWS_CAP:
+            if (value < 0) return HM_ERR_INVALID;
+            ctx->table_rows_cap = (uint64_t)value;
+            return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;
             ctx->grid_per_cu = (int)value;
@@ -921,9 +970,13 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<hm_result> res(n);
     for (auto& dv : ctx->devs) {
+        release_retired(dv);  // left by a call that failed mid-way
         dv.evnext = 0;
         dv.launches.clear();
     }
+    ctx->mid_syncs = 0;
+    ctx->table_grows = 0;
+    ctx->enqueue_ms = 0;
     uint64_t total = 0;
     for (int r = 0; r < n; ++r)
         if (reqs[r].lo <= reqs[r].hi) total += reqs[r].hi - reqs[r].lo + 1;  // wraps for 2^64
@@ -933,6 +986,8 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
         int rc = scan_chunk(ctx, reqs + c, m, res.data() + c, c == 0);
         if (rc) return rc;
     }
+    // every result is read back, so no work of the call is in flight
+    for (auto& dv : ctx->devs) release_retired(dv);
     const int ndev = (int)ctx->devs.size();
     // stats
     hm_stats st{};
@@ -996,6 +1051,9 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
         }
     }
     st.merge = ctx->merge;
+    st.enqueue_ms = ctx->enqueue_ms;
+    st.mid_call_syncs = ctx->mid_syncs;
+    st.table_grows = ctx->table_grows;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
                      .count();
     ctx->last = st;

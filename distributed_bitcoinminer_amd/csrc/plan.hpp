@@ -46,10 +46,11 @@ struct SegPlan {
 uint32_t digits_u64(uint64_t n);
 uint64_t pow10_u64(uint32_t k);  // k <= 19
 MsgPlan plan_message(const uint8_t* msg, uint64_t len);
-// Segment list for inclusive [lo, hi] (lo <= hi).  table_digits (1..6, 0 =
-// default 6) caps the final-block digits a chained K+W table covers; -1 turns
-// the chained layout of >= 5 final-block digits off (HM_OPT_TABLE_DIGITS, a
-// test hook: small tables make epochs on small ranges).
+// Segment list for inclusive [lo, hi] (lo <= hi).  table_digits (1..7, 0 =
+// default 7 = kTableDigits in plan.cpp) caps the final-block digits a chained
+// K+W table covers; -1 turns the chained layout of >= 5 final-block digits
+// off (HM_OPT_TABLE_DIGITS, a test hook: small tables make epochs on small
+// ranges).
 std::vector<SegPlan> plan_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, bool force_generic,
                                 int table_digits = 0);
 // Fraction of the nonces a chained layout hashes that lie in [s.lo, s.hi]: its

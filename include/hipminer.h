@@ -85,18 +85,32 @@ typedef struct hm_stats {
                                   minus the work hoisted out of the per-nonce
                                   loop.  Tiled: 1 (+1 with a constant trailer
                                   block); chained: 1 + 1/tch, the per-lane block
-                                  0 amortised over tch = min(10^f, 1000) loop
-                                  values (counted exactly per launch since ABI
+                                  0 amortised over tch loop values (f <= 4
+                                  final-block digits: tch = min(10^f, 1000);
+                                  f >= 5: tch = min(10^fe, 100), fe the table
+                                  digits) (counted exactly per launch since ABI
                                   1.5: one block-0 compression per task and
                                   lane, guided-split pieces included); generic:
                                   dom_compressions.  Mean over the dominant
                                   kernel's nonces (one instantiation may serve
                                   several segments). */
+    double enqueue_ms;       /* host time the call spent enqueuing GPU work on
+                                its devices (planning, K+W table allocation,
+                                launches) before it first waited (ABI 1.6)      */
+    int32_t mid_call_syncs;  /* host waits on GPU work issued while the call was
+                                still enqueuing work for some device (ABI 1.6;
+                                0: every device's work is queued before the
+                                host waits on any, so devices overlap)          */
+    int32_t table_grows;     /* chained K+W tables enlarged by the call; the
+                                old tables are freed after its results are read
+                                back, never mid-enqueue (ABI 1.6)               */
 } hm_stats;
 
 /* sizeof(hm_stats) by ABI version.  The struct only grows at its end. */
 #define HM_STATS_SIZE_1_0 136 /* ABI 1.0 .. 1.3                                 */
-#define HM_STATS_SIZE_1_4 144 /* ABI 1.4+: + dom_compressions_eff               */
+#define HM_STATS_SIZE_1_4 144 /* ABI 1.4, 1.5: + dom_compressions_eff          */
+#define HM_STATS_SIZE_1_6 160 /* ABI 1.6+: + enqueue_ms, mid_call_syncs,
+                                 table_grows                                     */
 
 #define HM_MERGE_NONE 0 /* one device: its result is read back directly      */
 #define HM_MERGE_HOST 1 /* several devices: 16-B results merged on the host  */
@@ -137,6 +151,12 @@ typedef struct hm_stats {
                                   values exercise the epochs on small ranges;
                                   -1 keeps final blocks of >= 5 digits on the
                                   tiled kernel (ABI 1.5)                        */
+#define HM_OPT_TABLE_ROWS_CAP 8 /* test hook (>= 0, 0 = off): a K+W table may not
+                                  grow beyond this many rows, as if the device
+                                  were out of memory; the chained layout then
+                                  falls back to smaller tables and more epochs
+                                  (the HM_ERR_NOMEM path of table growth; ABI
+                                  1.6)                                          */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */
@@ -192,9 +212,9 @@ int hm_partition(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int n
                  uint64_t *bounds);
 
 /* Stats of the last successful hm_scan / hm_scan_many on ctx.  Writes
- * sizeof(hm_stats) of THIS header (HM_STATS_SIZE_1_4 bytes): a caller built
- * against an older header (136-byte struct, ABI <= 1.3) must use
- * hm_scan_stats_sized instead, or check hm_version() >= 0x10004 first. */
+ * sizeof(hm_stats) of THIS header (HM_STATS_SIZE_1_6 bytes): a caller built
+ * against an older header (136 or 144 bytes, ABI <= 1.5) must use
+ * hm_scan_stats_sized instead, or check hm_version() >= 0x10006 first. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
 
 /* hm_scan_stats writing at most `size` bytes (pass sizeof(hm_stats) as the
@@ -210,6 +230,12 @@ void hm_close(hm_ctx *ctx);
 
 /* ABI version: (major << 16) | minor. */
 int hm_version(void);
+
+/* Build identity (ABI 1.6): 16 hex digits of sha256 over the sources the
+ * library was built from (distributed_bitcoinminer_amd/build_id.py: csrc/ and
+ * this header, by path and content).  A caller holding the source tree can
+ * check that the loaded library is that tree's build.  Static storage. */
+const char *hm_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,7 @@
 """The C-ABI library: loads, exports every symbol include/hipminer.h declares,
 host-side semantics (hm_hash), error handling.  No GPU compute here."""
 import ctypes
+import os
 
 import pytest
 
@@ -12,7 +13,7 @@ def test_exports_every_header_symbol():
     syms = _lib.header_symbols()
     assert set(syms) >= {"hm_hash", "hm_open", "hm_scan", "hm_scan_stats", "hm_set_option",
                          "hm_strerror", "hm_close", "hm_version", "hm_scan_checked",
-                         "hm_scan_many", "hm_partition", "hm_scan_stats_sized"}
+                         "hm_scan_many", "hm_partition", "hm_scan_stats_sized", "hm_build_id"}
     for s in syms:
         assert hasattr(lib, s), s
 
@@ -25,7 +26,7 @@ def test_library_is_gfx950_code_object():
 def test_version_and_strerror():
     lib = _lib.load()
     assert lib.hm_version() >> 16 == 1
-    assert lib.hm_version() & 0xFFFF >= 5  # 1.5: hm_scan_stats_sized
+    assert lib.hm_version() & 0xFFFF >= 6  # 1.6: hm_build_id, hm_stats.enqueue_ms ..
     for rc in range(0, -7, -1):
         assert _lib.strerror(rc)
     assert _lib.strerror(-99) == "unknown error"
@@ -78,22 +79,24 @@ def test_struct_layouts_match_header(tmp_path):
 
 def test_stats_size_is_pinned(tmp_path):
     """hm_stats only grows at its end: the 1.0-1.3 callers' 136-byte struct is
-    the prefix before dom_compressions_eff, the 1.4+ struct is 144 bytes, and
-    hm_scan_stats_sized refuses a size below the oldest layout."""
+    the prefix before dom_compressions_eff, the 1.4/1.5 struct the 144 bytes
+    before enqueue_ms, the 1.6 struct is 160 bytes, and hm_scan_stats_sized
+    refuses a size below the oldest layout."""
     import subprocess
     src = tmp_path / "sz.c"
     src.write_text("\n".join([
         '#include <stddef.h>', '#include <stdio.h>', f'#include "{_lib.HEADER_PATH}"',
         "int main(void) {",
-        '  printf("%zu %zu %d %d\\n", sizeof(hm_stats), offsetof(hm_stats, dom_compressions_eff),',
-        "         HM_STATS_SIZE_1_0, HM_STATS_SIZE_1_4);",
+        '  printf("%zu %zu %zu %d %d %d\\n", sizeof(hm_stats),',
+        "         offsetof(hm_stats, dom_compressions_eff), offsetof(hm_stats, enqueue_ms),",
+        "         HM_STATS_SIZE_1_0, HM_STATS_SIZE_1_4, HM_STATS_SIZE_1_6);",
         "  return 0;", "}"]))
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
     out = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
                                           text=True).stdout.split()]
-    assert out == [144, 136, 136, 144]
-    assert ctypes.sizeof(_lib.hm_stats) == 144
+    assert out == [160, 136, 144, 136, 144, 160]
+    assert ctypes.sizeof(_lib.hm_stats) == 160
     lib = _lib.load()
     st = _lib.hm_stats()
     assert lib.hm_scan_stats_sized(None, ctypes.byref(st), 144) == _lib.HM_ERR_INVALID
@@ -110,3 +113,38 @@ def test_code_object_hash_is_the_embedded_blob():
     if os.path.exists(hsaco):
         assert sha == hashlib.sha256(open(hsaco, "rb").read()).hexdigest()[:16]
     assert len(sha) == 16
+
+
+def test_build_id_is_this_trees_digest():
+    """hm_build_id (ABI 1.6) is the digest of the sources the library was built
+    from; the in-tree build matches this tree, the tag in the file's bytes
+    (what build() reads) equals what the loaded library returns, and the
+    digest covers every library source plus the header."""
+    from distributed_bitcoinminer_amd import build_id as bid
+    assert _lib.build_id() == bid.embedded_id(_lib.LIB_PATH)
+    assert _lib.build_matches_tree(), (_lib.build_id(), bid.tree_digest())
+    files = bid.source_files()
+    for f in ("api.cpp", "scan_kernels.hip", "kernels.hip", "plan.cpp", "sha_device.hpp",
+              "align_loops.py", "scan_blob.S", "Makefile"):
+        assert f"distributed_bitcoinminer_amd/csrc/{f}" in files, f
+    assert "include/hipminer.h" in files
+
+
+def test_build_id_changes_with_any_source(tmp_path):
+    """One changed byte in any covered source changes the digest."""
+    import shutil
+    from distributed_bitcoinminer_amd import build_id as bid
+    root = tmp_path / "tree"
+    for rel in bid.source_files():
+        dst = root / rel
+        dst.parent.mkdir(parents=True, exist_ok=True)
+        shutil.copyfile(os.path.join(bid.ROOT, rel), dst)
+    base = bid.tree_digest(str(root))
+    assert base == bid.tree_digest()
+    for rel in ("distributed_bitcoinminer_amd/csrc/scan_kernels.hip", "include/hipminer.h"):
+        p = root / rel
+        data = p.read_bytes()
+        p.write_bytes(data + b" ")
+        assert bid.tree_digest(str(root)) != base, rel
+        p.write_bytes(data)
+    assert bid.tree_digest(str(root)) == base

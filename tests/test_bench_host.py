@@ -86,3 +86,52 @@ def test_rounds_ops_of_the_tiled_kernel():
     ops_t, _ = bench.rounds_ops_per_nonce(dict(seg, W1=14, trailer=1), 2.0)
     ops_n, _ = bench.rounds_ops_per_nonce(dict(seg, W1=14), 1.0)
     assert abs(ops_t - ops_n - 64 * 16) < 1e-9
+
+
+def _full():
+    with open(os.path.join(ROOT, "tests", "golden", "full_size.json")) as f:
+        return json.load(f)
+
+
+def test_shard_check_weak_pieces_per_rank():
+    """Each weak-scaling rank r's own answer is checked against the fixture
+    piece [r*2^32, (r+1)*2^32) of its message (configs[1] and [2], r < 8)."""
+    for w in _full()["weak"]:
+        m = bytes.fromhex(w["msg_hex"])
+        for r, p in enumerate(w["pieces"]):
+            exp = (int(p["hash"]), int(p["nonce"]))
+            got = bench.shard_check(m, r << 32, ((r + 1) << 32) - 1, exp)
+            assert got["match"] is True and got["expected"]["nonce"] == exp[1], (w["name"], r)
+            bad = bench.shard_check(m, r << 32, ((r + 1) << 32) - 1, (exp[0], exp[1] + 1))
+            assert bad["match"] is False
+    # no fixture: a shard the pieces do not tile exactly, or another message
+    assert bench.shard_check(b"bradfitz", 5, (1 << 32) - 1, (1, 2)) is None
+    assert bench.shard_check(b"other", 0, (1 << 32) - 1, (1, 2)) is None
+    # an empty shard must answer the scan's seed
+    assert bench.shard_check(b"bradfitz", None, None, (bench.MAXU64, 0))["match"] is True
+    assert bench.shard_check(b"bradfitz", None, None, (5, 0))["match"] is False
+
+
+def test_shard_check_cfg4_partition_shards():
+    """configs[3]'s hm_partition shards for 1, 2, 4 and 8 ranks are unions of
+    the fixture's pieces, so every rank of the driver's strong-scaling run is
+    checked; their per-rank answers merge to the whole-range answer."""
+    from distributed_bitcoinminer_amd.parallel import shard_range
+    c4 = _full()["cfg4"]
+    whole = (int(c4["whole"]["hash"]), int(c4["whole"]["nonce"]))
+    for n in (1, 2, 4, 8):
+        exps = []
+        for r in range(n):
+            lo, hi = shard_range(0, (1 << 40) - 1, n, r, msg=b"bradfitz")
+            inside = [p for p in c4["pieces"] if int(p["lo"]) >= lo and int(p["hi"]) <= hi]
+            exp = min((int(p["hash"]), int(p["nonce"])) for p in inside)
+            got = bench.shard_check(b"bradfitz", lo, hi, exp)
+            assert got is not None and got["match"] is True, (n, r)
+            exps.append(exp)
+        assert min(exps) == whole
+
+
+def test_all_match():
+    assert bench.all_match({"match": [True, True]}) is True
+    assert bench.all_match({"match": [True, False, None]}) is False
+    assert bench.all_match({"match": [True, None]}) is None

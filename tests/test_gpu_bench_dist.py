@@ -48,13 +48,32 @@ def _torchrun(nproc, args, env_extra, timeout):
     return json.loads(lines[0])
 
 
+def _per_rank(ranks, n, ordinals=None):
+    """Every rank reports its own answer, device and kernel rate, and its
+    answer equals the fixture piece(s) of its own shard."""
+    assert ranks["match"] == [True] * n, ranks
+    assert len(ranks["answer"]) == n and len(ranks["device"]) == n
+    assert all(g > 0 for g in ranks["kernel_GHs"]), ranks["kernel_GHs"]
+    if ordinals is not None:
+        assert [d["ordinal"] for d in ranks["device"]] == ordinals
+    assert all(len(d["pci_bus_id"]) == 12 for d in ranks["device"]), ranks["device"]
+
+
 def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
     line = _torchrun(2, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
                          "--no-cpu-baseline"], {"HM_BENCH_BACKEND": "gloo"}, timeout=420)
     assert line["n_gpus"] == 2 and line["config"]["merge"] == "gloo"
     assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
     assert len(line["ranks"]["local_ms"]) == 2
+    assert line["build_matches_tree"] is True, line["build_id"]
+    assert line["all_ranks_match"] is True
+    _per_rank(line["ranks"], 2, [0, 0])  # gloo rehearsal: both ranks on GPU 0
+    # the merged answer is the minimum of the ranks' own answers
+    best = min((a["hash"], a["nonce"]) for a in line["ranks"]["answer"])
+    assert best == (line["result"]["hash"], line["result"]["nonce"])
     c4 = line["workloads"]["cfg4"]
+    assert c4["all_ranks_match"] is True
+    _per_rank(c4["ranks"], 2, [0, 0])
     assert c4["scaling"] == "strong"
     assert c4["result_vs_oracle"]["fixture"] == "tests/golden/full_size.json"
     assert c4["result_vs_oracle"]["match"] is True, c4["result_vs_oracle"]
@@ -70,7 +89,10 @@ def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
                          "--no-cpu-baseline"], {"HM_BENCH_FORCE_DIST": "1"}, timeout=300)
     assert line["config"]["merge"] == "RCCL all-gather"
     assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
+    assert line["all_ranks_match"] is True and line["build_matches_tree"] is True
+    _per_rank(line["ranks"], 1, [0])
     c3 = line["workloads"]["cfg3"]
+    assert c3["all_ranks_match"] is True
     assert c3["result_vs_oracle"]["match"] is True, c3["result_vs_oracle"]
     rl = c3["roofline"]
     assert rl["kernel"] == "hm_chained_kernel"
@@ -93,3 +115,9 @@ def test_bench_torchrun_rccl_all_visible_gpus():
     c4 = line["workloads"]["cfg4"]
     assert c4["result_vs_oracle"]["match"] is True, c4["result_vs_oracle"]
     assert len(line["ranks"]["local_ms"]) == n and len(c4["ranks"]["local_ms"]) == n
+    # one rank per GPU: distinct ordinals and PCI addresses, each rank's own
+    # shard equal to its fixture piece (n <= 8: every rank has one)
+    _per_rank(line["ranks"], n, list(range(n)))
+    _per_rank(c4["ranks"], n, list(range(n)))
+    assert len({d["pci_bus_id"] for d in line["ranks"]["device"]}) == n
+    assert line["all_ranks_match"] is True and c4["all_ranks_match"] is True

@@ -211,6 +211,35 @@ def test_rccl_merge_distinct_devices(oracle_mod):
         assert c.scan(b"bradfitz", 5, 4) == (MAX, 0)
 
 
+def test_config4_single_process_rccl_all_gpus():
+    """configs[3] through the process model SURVEY §8(e) prescribes for one
+    miner driving every GPU: one context over all visible devices
+    (ncclCommInitAll over distinct ordinals), "bradfitz" [0, 2^40) sharded by
+    hm_partition, the 16-B results merged by the grouped RCCL all-gather and
+    the device fold.  The answer is full_size.json's whole-range oracle answer;
+    the devices ran concurrently (summed kernel busy time well above the wall
+    time) and the host never waited mid-enqueue.  Needs >= 2 GPUs."""
+    import json
+    import os
+    import torch
+    n = min(torch.cuda.device_count(), 8)
+    if n < 2:
+        pytest.skip(f"{n} visible GPU(s): the single-process RCCL context needs >= 2")
+    with open(os.path.join(os.path.dirname(__file__), "golden", "full_size.json")) as f:
+        w = json.load(f)["cfg4"]["whole"]
+    exp = (int(w["hash"]), int(w["nonce"]))
+    with _lib.Context(list(range(n))) as c:
+        c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+        assert c.scan(b"bradfitz", 0, (1 << 40) - 1) == exp
+        st = c.stats()
+        assert st["merge"] == _lib.HM_MERGE_RCCL and st["ndev"] == n, st
+        assert st["mid_call_syncs"] == 0, st
+        assert st["kernel_ms"] > 0.6 * n * st["wall_ms"], st  # devices overlapped
+        print(f"cfg4 on {n} GPUs, one process: wall {st['wall_ms']:.1f} ms = "
+              f"{(1 << 40) / st['wall_ms'] / 1e6:.1f} GH/s; kernel "
+              f"{(1 << 40) / (st['kernel_ms'] / n) / 1e6:.1f} GH/s")
+
+
 def test_miner_eval_request_on_gpu(ctx, golden):
     from distributed_bitcoinminer_amd import bitcoin, miner
     mnr = miner.Miner(ctx=ctx)
