@@ -241,6 +241,20 @@ std::vector<Shard> partition_range(const MsgPlan& mp, uint64_t lo, uint64_t hi, 
             if (k < 0) k = 0;
             const u128 kk = k > (long double)cnt_m1 ? (u128)cnt_m1 + 1 : (u128)(uint64_t)k;
             b = (u128)(segs[si].lo - lo) + kk;
+            const SegPlan& g = segs[si];
+            if (g.kind == HM_KIND_CHAINED && g.f >= 5 && kk > 0 && kk <= cnt_m1) {
+                // A chained f >= 5 lane chunk spans 64 * 10^f nonces (lanes
+                // stride 10^f) and is hashed whole by every shard that touches
+                // it: a cut inside one would hash it twice.  Cut at the nearest
+                // lane-chunk boundary of the tile instead (at most half a
+                // chunk away from the cost target).
+                const u128 x = (u128)lo + b;  // the next shard's first nonce
+                const u128 P = g.pow10V, C = (u128)64 * pow10_u64(g.f);
+                const u128 t0 = x / P * P;
+                const u128 c = (x - t0 + C / 2) / C;
+                const u128 snapped = t0 + std::min(c * C, P);
+                if (snapped > (u128)g.lo && snapped <= (u128)g.hi) b = snapped - lo;
+            }
         }
         start[i] = std::min(count, std::max(b, start[i - 1]));
     }

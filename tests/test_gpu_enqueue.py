@@ -53,8 +53,8 @@ def test_table_growth_does_not_block_enqueue(oracle_mod):
         st = c.stats()
         assert st["ndev"] == 2
         assert st["mid_call_syncs"] == 0, st
-        # each device's shard of F5 and of F6 grows a table (>= 2 per device)
-        assert st["table_grows"] >= 4, st
+        # both devices' chained shards grow tables beyond the 10^4 rows of hm_open
+        assert st["table_grows"] >= 2, st
         # ~0.5 s of kernels; enqueuing (planning, 10^5/10^6-row allocations,
         # launches) must not have waited for them
         assert st["kernel_ms"] > 200, st

@@ -93,3 +93,38 @@ def test_shard_range_with_msg_uses_partition():
     for r in range(8):
         assert parallel.shard_range(0, 2**32 - 1, 8, r, msg=b"a" * 45) == \
             _lib.partition(b"a" * 45, 0, 2**32 - 1, 8)[r]
+
+
+def _chunk_bounds(seg):
+    """Lane-chunk boundaries of a chained segment: tile t's chunk c starts at
+    t*10^(q+f) + c*64*10^f (lanes vary block-0 digits, stride 10^f)."""
+    P = 10 ** (seg["V"])
+    C = 64 * 10 ** seg["f"]
+    return P, C
+
+
+@pytest.mark.parametrize("msg,lo,hi", [(b"x" * 60, 10**9, 10**10 - 1),
+                                       (b"y" * 58, 10**10 + 77_777_777, 10**10 + 2_277_777_777)])
+def test_partition_cuts_chained_f5_at_lane_chunks(msg, lo, hi):
+    """A chained f >= 5 lane chunk spans 64*10^f nonces and is hashed whole by
+    each shard that touches it, so hm_partition cuts such segments at lane
+    chunk boundaries (plan.cpp partition_range): every internal cut is one,
+    each shard still re-plans as the chained layout, and the shards' modelled
+    costs (re-planned, edge lanes included) stay within one chunk of each
+    other and add up to the whole range's."""
+    seg = _lib.debug_plan(msg, lo, hi)[0]
+    assert seg["kind"] == _lib.HM_KIND_CHAINED and seg["f"] >= 5
+    P, C = _chunk_bounds(seg)
+    chunk_cost = C * seg["cost"]  # one lane chunk's nonces x their per-nonce cost
+    whole = _shard_cost(msg, (lo, hi))
+    for n in (2, 4, 8):
+        shards = _lib.partition(msg, lo, hi, n)
+        _check_cover(shards, lo, hi)
+        for a, _ in shards[1:]:
+            assert (a % P) % C == 0, (n, a)
+        # shards between two cuts hold whole chunks: the chained layout stays
+        for s in shards[1:-1]:
+            assert all(p["kind"] == _lib.HM_KIND_CHAINED for p in _lib.debug_plan(msg, *s)), s
+        costs = [_shard_cost(msg, s) for s in shards]
+        assert max(costs) - min(costs) <= 1.05 * chunk_cost, (n, costs, chunk_cost)
+        assert sum(costs) <= 1.02 * whole, (n, sum(costs), whole)
