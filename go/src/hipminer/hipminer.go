@@ -180,3 +180,10 @@ func Partition(data string, lo, hi uint64, n int) ([][2]uint64, error) {
 	}
 	return out, nil
 }
+
+// BuildID is hm_build_id(): the digest of the sources libhipminer.so was built
+// from (distributed_bitcoinminer_amd/build_id.py), for start-up logs and
+// deployment checks.
+func BuildID() string {
+	return C.GoString(C.hm_build_id())
+}

@@ -69,10 +69,12 @@ def test_table_growth_does_not_block_enqueue(oracle_mod):
 
 def test_single_device_growth_on_second_stream(oracle_mod):
     """One device: a large request keeps stream 0 busy while the chained
-    requests' segments grow the tables of the other streams."""
-    reqs = [(b"bradfitz", 0, (2 << 32) - 1), F6, F5]
+    requests grow K+W tables: F5 (small, round-robin stream) to 10^5 rows,
+    then F6 (2.2e8 nonces: the dominant-stream order, stream 0) to 10^6 rows,
+    which retires a table still in use if F5 went to stream 0 too."""
+    reqs = [(b"bradfitz", 0, (2 << 32) - 1), F5, F6]
     exp = [_weak_prefix(2)] + [oracle_mod.fast_scan_sum(m, lo, hi, threads=THREADS)[0]
-                               for m, lo, hi in (F6, F5)]
+                               for m, lo, hi in (F5, F6)]
     with _lib.Context([0]) as c:
         assert c.scan_many(reqs) == exp
         st = c.stats()
