@@ -9,6 +9,8 @@ random digit-count boundaries or anywhere, from 1 to ~2*10^6 nonces, some
 ending at 2^64-1.  One case in five is a two-block tail with 5 final-block
 digits over 1.3-3.2*10^7 nonces (the chained layout with a K+W table, round 3)
 under a random table cap HM_OPT_TABLE_DIGITS (1..5: 10^4..1 epochs).
+A second soak (half the budget) sends random hm_scan_many batches to fresh
+multi-"device" contexts under random stream counts and table-growth caps.
 HM_SOAK_SEED picks the sequence; a failure names its case.
 Progress goes to stdout every ~10 s (run with -s).
 """
@@ -76,4 +78,51 @@ def test_random_soak_checked(ctx, oracle_mod):
             last = time.time()
             print(f"soak: {n} cases, {nonces} nonces, {last - t0:.0f} s", flush=True)
     print(f"soak done: seed {seed}, {n} cases, {nonces} nonces, all equal to the oracle", flush=True)
+    assert n > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(3600)
+def test_random_batches_fresh_contexts(oracle_mod):
+    """Randomised hm_scan_many batches on fresh contexts (round 4): 1..3
+    "devices" (GPU 0 opened repeatedly, so the batch is sharded and each shard
+    grows its own K+W tables), 1 or 4 streams, a random HM_OPT_TABLE_ROWS_CAP
+    (growth refused above 10^4 / 10^5 rows, as on a device out of memory) and
+    2..6 requests mixing the random cases with chained f = 5 cases.  Tables
+    grow while earlier requests' work is in flight and are freed after the
+    readback; every answer equals the oracle's.  Runs for HM_SOAK_SECONDS / 2."""
+    from distributed_bitcoinminer_amd import _lib
+    budget = float(os.environ.get("HM_SOAK_SECONDS", "20")) / 2
+    seed = int(os.environ.get("HM_SOAK_SEED", "355")) + 1
+    rng = random.Random(seed)
+    t0 = last = time.time()
+    n = reqs_done = grows = 0
+    while time.time() - t0 < budget:
+        devs = [0] * rng.randrange(1, 4)
+        streams = rng.choice([1, 4])
+        cap = rng.choice([0, 0, 10**4, 10**5])
+        reqs = []
+        for _ in range(rng.randrange(2, 7)):
+            if rng.randrange(3) == 0:
+                m, lo, hi, _ = _epoch_case(rng)
+            else:
+                m, lo, hi = _case(rng)
+            reqs.append((m, lo, hi))
+        exp = [tuple(oracle_mod.fast_scan_sum(m, lo, hi, threads=16)[0]) for m, lo, hi in reqs]
+        with _lib.Context(devs) as c:
+            c.set_option(_lib.HM_OPT_STREAMS, streams)
+            c.set_option(_lib.HM_OPT_TABLE_ROWS_CAP, cap)
+            got = c.scan_many(reqs)
+            st = c.stats()
+        assert got == exp, (n, len(devs), streams, cap, [(m.hex(), lo, hi) for m, lo, hi in reqs])
+        assert st["mid_call_syncs"] == 0, (n, st)
+        n += 1
+        reqs_done += len(reqs)
+        grows += st["table_grows"]
+        if time.time() - last > 10:
+            last = time.time()
+            print(f"batch soak: {n} batches, {reqs_done} requests, {grows} table growths, "
+                  f"{last - t0:.0f} s", flush=True)
+    print(f"batch soak done: seed {seed}, {n} batches, {reqs_done} requests, {grows} table "
+          f"growths, all equal to the oracle", flush=True)
     assert n > 0
