@@ -83,3 +83,19 @@ def test_full_size_fixtures_agree_at_2p32():
         assert (p["lo"], p["hi"]) == (c["lo"], c["hi"]) == ("0", str(2**32 - 1))
         for k in ("hash", "nonce", "sum", "count"):
             assert p[k] == c[k], (w["name"], k)
+
+
+def test_fast_oracle_long_messages(oracle_mod):
+    """The fast oracle's midstate over many constant blocks (the long-message
+    GPU tests' checker) against the per-nonce oracle, lengths up to 64 KiB."""
+    import random
+    if not oracle_mod.fast_available():
+        import pytest
+        pytest.skip("no SHA extensions on this host")
+    for L in (255, 256, 1983, 4096, 65537):
+        rng = random.Random(L)
+        m = bytes(rng.randrange(256) for _ in range(L))
+        for lo in (10**9 - 300, (1 << 64) - 400):
+            hi = min((1 << 64) - 1, lo + 399)
+            assert oracle_mod.fast_scan_sum(m, lo, hi, threads=2) == \
+                oracle_mod.c_scan_sum(m, lo, hi), (L, lo)
