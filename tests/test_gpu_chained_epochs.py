@@ -147,3 +147,28 @@ def test_batches_streams_and_devices(oracle_mod):
             c.set_option(_lib.HM_OPT_STREAMS, streams)
             assert c.scan_many(reqs) == exp, (devs, streams)
             assert [c.scan(m, lo, hi) for m, lo, hi in reqs] == exp, (devs, streams)
+
+
+def test_shards_cut_at_lane_chunks_checked(oracle_mod):
+    """Multi-device contexts (GPU 0 opened 3 and 5 times) shard chained f >= 5
+    ranges with hm_partition, whose cuts now fall on lane-chunk boundaries
+    (plan.cpp partition_range): every shard re-plans as the chained layout and
+    the per-device checked scans still cover the range exactly -- (min, key
+    sum, count) equal the oracle's, so no nonce is lost or doubled at a cut."""
+    m58 = bytes(random.Random(58).randrange(33, 127) for _ in range(58))
+    m60 = bytes(random.Random(60).randrange(33, 127) for _ in range(60))
+    cases = [(m58, 10**9 + 1_234_567, 10**9 + 71_234_567),      # f = 5, q = 5
+             (m60, 10**7 + 5, 10**8 - 7),                        # f = 5, q = 3
+             (m58, 10**10 + 3, 10**10 + 300_000_003)]            # f = 6
+    for m, lo, hi in cases:
+        exp = oracle_mod.fast_scan_sum(m, lo, hi, threads=THREADS)
+        seg = _lib.debug_plan(m, lo, hi)[0]
+        P, C = 10 ** seg["V"], 64 * 10 ** seg["f"]
+        for n in (3, 5):
+            cuts = [a for a, _ in _lib.partition(m, lo, hi, n)[1:]]
+            assert all((a % P) % C == 0 for a in cuts), (n, cuts)
+            with _lib.Context([0] * n) as c:
+                assert c.scan_checked(m, lo, hi) == exp, (len(m), lo, hi, n)
+                assert c.stats()["ndev"] == n
+                assert c.scan(m, lo, hi) == exp[0]
+                assert c.stats()["dom_kernel"] == "hm_chained_kernel"
