@@ -85,7 +85,7 @@ struct Device {
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
     uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
-    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed after the call
+    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed at hm_close
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
@@ -353,9 +353,11 @@ int host_wait(hm_ctx* ctx, hipStream_t st) {
 // Make stream si's K+W table hold `rows` rows.  Grown once to the largest
 // table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of
 // >= 5 digits).  Work queued earlier on any stream may still read the old
-// table, so it is not freed here (hipFree waits for the device): it is
-// retired and freed after the call's results are read back
-// (release_retired), and the host never blocks mid-enqueue.
+// table, and hipFree would wait for the whole device (other contexts' work
+// on it included), so the old table is retired, not freed: the host never
+// blocks, mid-enqueue or after.  Retired tables are freed at hm_close.  Rows
+// are powers of ten and only grow, so a stream's retired tables hold less
+// than 1/9 of its current one (at most 0.28 GB beside a 10^7-row table).
 // Returns HM_ERR_NOMEM (with HIP's error state cleared, the old table kept)
 // when the device cannot hold the table, or the HM_OPT_TABLE_ROWS_CAP test
 // hook refuses it; the caller then plans smaller tables.
@@ -372,15 +374,6 @@ int kw_table_rows(hm_ctx* ctx, Device& dv, int si, uint64_t rows) {
     dv.kwt_rows[si] = rows;
     ++ctx->table_grows;
     return HM_OK;
-}
-
-// Free the tables kw_table_rows retired.  Called between calls only (no work
-// of this context in flight), since hipFree synchronises the device.
-void release_retired(Device& dv) {
-    if (dv.retired.empty()) return;
-    (void)hipSetDevice(dv.ordinal);
-    for (uint32_t* t : dv.retired) (void)hipFree(t);
-    dv.retired.clear();
 }
 
 // One chained launch: tiles [t, t + nt) of segment s in epoch e (final-block
@@ -970,7 +963,6 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
     const auto t0 = std::chrono::steady_clock::now();
     std::vector<hm_result> res(n);
     for (auto& dv : ctx->devs) {
-        release_retired(dv);  // left by a call that failed mid-way
         dv.evnext = 0;
         dv.launches.clear();
     }
@@ -986,8 +978,6 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
         int rc = scan_chunk(ctx, reqs + c, m, res.data() + c, c == 0);
         if (rc) return rc;
     }
-    // every result is read back, so no work of the call is in flight
-    for (auto& dv : ctx->devs) release_retired(dv);
     const int ndev = (int)ctx->devs.size();
     // stats
     hm_stats st{};

@@ -101,9 +101,10 @@ typedef struct hm_stats {
                                 still enqueuing work for some device (ABI 1.6;
                                 0: every device's work is queued before the
                                 host waits on any, so devices overlap)          */
-    int32_t table_grows;     /* chained K+W tables enlarged by the call; the
-                                old tables are freed after its results are read
-                                back, never mid-enqueue (ABI 1.6)               */
+    int32_t table_grows;     /* chained K+W tables enlarged by the call; an old
+                                table may still be read by queued work, so it
+                                is kept (< 1/9 of the new one) until hm_close:
+                                growth never waits on the device (ABI 1.6)      */
 } hm_stats;
 
 /* sizeof(hm_stats) by ABI version.  The struct only grows at its end. */

@@ -1,9 +1,9 @@
 """The host never waits on the GPU while a call is still enqueuing (ABI 1.6).
 
 Chained f >= 5 segments grow their stream's K+W table (10^5 .. 10^7 rows).
-Work queued earlier may still read the old table, so it is retired and freed
-after the call's results are read back (api.cpp kw_table_rows /
-release_retired) instead of draining the device mid-enqueue: every device of a
+Work queued earlier may still read the old table, so it is retired (kept
+until hm_close, api.cpp kw_table_rows) instead of freed, which would drain
+the device mid-enqueue: every device of a
 context gets its work before the host waits on any of it (one
 context drives all of a miner's GPUs).  hm_stats counts the waits issued while
 enqueuing (mid_call_syncs), the tables grown (table_grows) and the host time

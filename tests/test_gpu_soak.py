@@ -89,8 +89,8 @@ def test_random_batches_fresh_contexts(oracle_mod):
     grows its own K+W tables), 1 or 4 streams, a random HM_OPT_TABLE_ROWS_CAP
     (growth refused above 10^4 / 10^5 rows, as on a device out of memory) and
     2..6 requests mixing the random cases with chained f = 5 cases.  Tables
-    grow while earlier requests' work is in flight and are freed after the
-    readback; every answer equals the oracle's.  Runs for HM_SOAK_SECONDS / 2."""
+    grow while earlier requests' work is in flight (the old ones are retired
+    until the context closes); every answer equals the oracle's.  Runs for HM_SOAK_SECONDS / 2."""
     from distributed_bitcoinminer_amd import _lib
     budget = float(os.environ.get("HM_SOAK_SECONDS", "20")) / 2
     seed = int(os.environ.get("HM_SOAK_SEED", "355")) + 1
