@@ -96,7 +96,8 @@ typedef struct hm_stats {
                                   several segments). */
     double enqueue_ms;       /* host time the call spent enqueuing GPU work on
                                 its devices (planning, K+W table allocation,
-                                launches) before it first waited (ABI 1.6)      */
+                                launches) before waiting for results, summed
+                                over its chunks of <= 64 requests (ABI 1.6)     */
     int32_t mid_call_syncs;  /* host waits on GPU work issued while the call was
                                 still enqueuing work for some device (ABI 1.6;
                                 0: every device's work is queued before the
