@@ -139,6 +139,41 @@ def shard_check(msg: bytes, lo, hi, res):
     return None
 
 
+def single_process_cfg4(devices, rccl: bool):
+    """configs[3] ([0, 2^40) of "bradfitz") through ONE process driving every
+    device in `devices` -- SURVEY §8(e)'s own process model (one hm_open over
+    the device list, hm_partition shards, 16-B results merged on the host, or
+    with the in-library RCCL all-gather when `rccl`).  Timed once after a
+    small untimed warm-up scan; checked against full_size.json's whole-range
+    answer.  Never raises: a failure is reported in the returned dict."""
+    from distributed_bitcoinminer_amd import _lib
+    m, hi = WORKLOADS["cfg4"][0], (1 << 40) - 1
+    try:
+        with _lib.Context(devices) as c:
+            if rccl:
+                c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+            c.scan(m, 0, 10**9)  # module load, first launches, RCCL communicator
+            t = time.perf_counter()
+            res = c.scan(m, 0, hi)
+            el = time.perf_counter() - t
+            st = c.stats()
+    except Exception as e:  # reported, never fatal to the bench line
+        return {"devices": list(devices), "error": f"{type(e).__name__}: {e}"}
+    merge = {_lib.HM_MERGE_NONE: "none", _lib.HM_MERGE_HOST: "host",
+             _lib.HM_MERGE_RCCL: "RCCL all-gather"}.get(st["merge"], str(st["merge"]))
+    return {"workload": "cfg4 in one process: hm_open over every GPU, [0, 2^40) as "
+                        "hm_partition shards, 16-B results merged (SURVEY 8(e))",
+            "devices": list(devices), "merge": merge,
+            "value": round((hi + 1) / el / 1e9, 3), "unit": "GH/s", "wall_ms": round(el * 1e3, 3),
+            # kernel_ms sums the devices' busy time: nonces / it = the mean
+            # per-device kernel rate
+            "kernel_GHs_per_device": round((hi + 1) / st["kernel_ms"] / 1e6, 3)
+            if st["kernel_ms"] > 0 else None,
+            "enqueue_ms": round(st["enqueue_ms"], 3), "mid_call_syncs": st["mid_call_syncs"],
+            "result": {"hash": res[0], "nonce": res[1]},
+            "result_vs_oracle": fixture_check(m, 0, hi, res)}
+
+
 def all_match(ranks):
     """True when every rank's answer equals its fixture piece, False when any
     differs, None when some rank has no fixture (and none differs)."""
@@ -573,6 +608,24 @@ def main():
                 "all_ranks_match": all_match(rk2),
                 "roofline": roofline(st2, m2, lo2, hi2) if lo2 is not None else None}
 
+    # configs[3] once more through SURVEY §8(e)'s single-process model, on a
+    # multi-GPU run (rank 0 drives every GPU while the other ranks wait at the
+    # barrier, after every timed region above).  HM_BENCH_SP_DEVICES (e.g.
+    # "0,0") runs it on a 1-GPU box too; HM_BENCH_SP_RCCL=1 merges with RCCL.
+    sp_env = os.environ.get("HM_BENCH_SP_DEVICES")
+    sp_devices = [int(x) for x in sp_env.split(",")] if sp_env else \
+        (list(range(world)) if world > 1 and backend == "nccl" else None)
+    single = None
+    if sp_devices and "cfg4" in names:
+        barrier()
+        if rank == 0:
+            seen = torch.cuda.device_count()
+            if max(sp_devices) >= seen:
+                single = {"devices": sp_devices, "skipped": f"rank 0 sees {seen} GPU(s)"}
+            else:
+                single = single_process_cfg4(sp_devices, os.environ.get("HM_BENCH_SP_RCCL") == "1")
+        barrier()
+
     if rank == 0:
         total = total_nonces * args.steps
         value = total / elapsed / 1e9
@@ -604,13 +657,16 @@ def main():
         }
         if secondary:
             line["workloads"] = secondary
+        if single is not None:
+            line["single_process"] = single
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(msg, args.workload)
             line["cpu_baseline"] = cb
         os.write(json_fd, (json.dumps(line) + "\n").encode())
         # a wrong answer fails the run (after the line is out, so the
         # mismatching rank and device are on record)
-        checks = [line["result_vs_oracle"], *(w["result_vs_oracle"] for w in secondary.values())]
+        checks = [line["result_vs_oracle"], *(w["result_vs_oracle"] for w in secondary.values()),
+                  (single or {}).get("result_vs_oracle")]
         wrong = [c for c in checks if c is not None and c["match"] is False]
         wrong += [n for n, rk in [("primary", ranks)] + [(k, w["ranks"]) for k, w in secondary.items()]
                   if all_match(rk) is False]

@@ -121,3 +121,27 @@ def test_bench_torchrun_rccl_all_visible_gpus():
     _per_rank(c4["ranks"], n, list(range(n)))
     assert len({d["pci_bus_id"] for d in line["ranks"]["device"]}) == n
     assert line["all_ranks_match"] is True and c4["all_ranks_match"] is True
+    # configs[3] again through one process driving all n GPUs
+    sp = line["single_process"]
+    assert sp["devices"] == list(range(n)) and sp["merge"] == "host", sp
+    assert sp["result_vs_oracle"]["match"] is True and sp["mid_call_syncs"] == 0, sp
+
+
+def test_bench_single_process_workload_on_one_gpu():
+    """bench.py's single-process configs[3] measurement (the line's
+    `single_process`, taken on multi-GPU runs) exercised on a 1-GPU box:
+    HM_BENCH_SP_DEVICES=0,0 opens GPU 0 twice, so the hm_partition shards,
+    the per-device enqueue and the host merge of a 2-device context run on
+    [0, 2^40), and the answer equals full_size.json's."""
+    env = dict(os.environ, HM_BENCH_SP_DEVICES="0,0")
+    cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--secondary", "cfg4",
+           "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, p.stderr[-4000:]
+    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    sp = line["single_process"]
+    assert "error" not in sp and "skipped" not in sp, sp
+    assert sp["devices"] == [0, 0] and sp["merge"] == "host"
+    assert sp["result_vs_oracle"]["match"] is True, sp
+    assert sp["result"] == line["workloads"]["cfg4"]["result"]
+    assert sp["mid_call_syncs"] == 0 and sp["value"] > 0
