@@ -88,7 +88,8 @@ def test_random_batches_fresh_contexts(oracle_mod):
     "devices" (GPU 0 opened repeatedly, so the batch is sharded and each shard
     grows its own K+W tables), 1 or 4 streams, a random HM_OPT_TABLE_ROWS_CAP
     (growth refused above 10^4 / 10^5 rows, as on a device out of memory) and
-    2..6 requests mixing the random cases with chained f = 5 cases.  Tables
+    2..6 requests (one batch in ten: 65..80, two hm_scan_many chunks) mixing
+    the random cases with chained f = 5 cases.  Tables
     grow while earlier requests' work is in flight (the old ones are retired
     until the context closes); every answer equals the oracle's.  Runs for HM_SOAK_SECONDS / 2."""
     from distributed_bitcoinminer_amd import _lib
@@ -102,7 +103,8 @@ def test_random_batches_fresh_contexts(oracle_mod):
         streams = rng.choice([1, 4])
         cap = rng.choice([0, 0, 10**4, 10**5])
         reqs = []
-        for _ in range(rng.randrange(2, 7)):
+        # one batch in ten spans two hm_scan_many chunks (> kMaxBatch = 64)
+        for _ in range(rng.randrange(65, 81) if rng.randrange(10) == 0 else rng.randrange(2, 7)):
             if rng.randrange(3) == 0:
                 m, lo, hi, _ = _epoch_case(rng)
             else:
