@@ -29,6 +29,14 @@ dominant scan launch / its HIP-event duration (measured live, on the stream
 the kernel runs on); peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz.
 `frac_rounds` prices instead the rounds and schedule words the kernel's
 formulation executes per nonce (rounds_ops_per_nonce).
+Per-rank self-check: every workload's `ranks` carries each rank's own 16-B
+answer, its device (ordinal, PCI address) and kernel GH/s, and `match` of
+that answer against the fixture pieces tiling the rank's shard
+(tests/golden/full_size.json); `all_ranks_match` sums them up.  Any mismatch
+exits 1 after the line is printed.  `build_id` / `build_matches_tree` tie the
+measured library to the sources beside this file.
+single_process (multi-GPU runs): configs[3] once more through ONE process
+driving every GPU (SURVEY §8(e)'s process model), after every timed region.
 cpu_baseline: the reference miner fleet restated on the host -- one thread
 per core of this process's CPU share (<= 16), each a sequential miner over
 its own chunk, running the C restatement of the reference loop
