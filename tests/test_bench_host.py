@@ -135,3 +135,15 @@ def test_all_match():
     assert bench.all_match({"match": [True, True]}) is True
     assert bench.all_match({"match": [True, False, None]}) is False
     assert bench.all_match({"match": [True, None]}) is None
+
+
+def test_single_process_failure_is_reported_not_raised():
+    """bench.single_process_cfg4 runs after every timed region of a multi-GPU
+    line; a failure there (here: no GPU, hm_open fails) must land in the line,
+    never abort the run that prints it."""
+    import torch
+    if torch.cuda.is_available():
+        import pytest
+        pytest.skip("GPU present")
+    out = bench.single_process_cfg4([0, 1], rccl=True)
+    assert out["devices"] == [0, 1] and "HipMinerError" in out["error"]
