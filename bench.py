@@ -625,6 +625,14 @@ def main():
         (list(range(world)) if world > 1 and backend == "nccl" else None)
     single = None
     if sp_devices and "cfg4" in names:
+        # the other ranks wait on the host (a gloo group), so no RCCL barrier
+        # kernel spins on their GPUs while rank 0 measures on them
+        wait_group = None
+        if dist is not None:
+            try:
+                wait_group = dist.new_group(backend="gloo")
+            except Exception:  # no gloo: the default (device) barrier
+                wait_group = None
         barrier()
         if rank == 0:
             seen = torch.cuda.device_count()
@@ -632,6 +640,8 @@ def main():
                 single = {"devices": sp_devices, "skipped": f"rank 0 sees {seen} GPU(s)"}
             else:
                 single = single_process_cfg4(sp_devices, os.environ.get("HM_BENCH_SP_RCCL") == "1")
+        if wait_group is not None:
+            dist.barrier(group=wait_group)
         barrier()
 
     if rank == 0:

@@ -132,13 +132,14 @@ def test_bench_single_process_workload_on_one_gpu():
     `single_process`, taken on multi-GPU runs) exercised on a 1-GPU box:
     HM_BENCH_SP_DEVICES=0,0 opens GPU 0 twice, so the hm_partition shards,
     the per-device enqueue and the host merge of a 2-device context run on
-    [0, 2^40), and the answer equals full_size.json's."""
-    env = dict(os.environ, HM_BENCH_SP_DEVICES="0,0")
-    cmd = [sys.executable, "bench.py", "--steps", "1", "--warmup", "0", "--secondary", "cfg4",
-           "--no-cpu-baseline"]
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
-    assert p.returncode == 0, p.stderr[-4000:]
-    line = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][0])
+    [0, 2^40), and the answer equals full_size.json's.  Launched as the
+    driver launches bench.py (torch.distributed.run, RCCL process group at
+    world size 1 via HM_BENCH_FORCE_DIST), so the host-side (gloo) wait group
+    the other ranks park on is created and used too."""
+    line = _torchrun(1, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
+                         "--no-cpu-baseline"],
+                     {"HM_BENCH_FORCE_DIST": "1", "HM_BENCH_SP_DEVICES": "0,0"}, timeout=400)
+    assert line["config"]["merge"] == "RCCL all-gather"
     sp = line["single_process"]
     assert "error" not in sp and "skipped" not in sp, sp
     assert sp["devices"] == [0, 0] and sp["merge"] == "host"
