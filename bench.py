@@ -625,8 +625,11 @@ def main():
         (list(range(world)) if world > 1 and backend == "nccl" else None)
     single = None
     if sp_devices and "cfg4" in names:
-        # the other ranks wait on the host (a gloo group), so no RCCL barrier
-        # kernel spins on their GPUs while rank 0 measures on them
+        # every rank's own context is done: closing it releases its HIP
+        # streams (hardware queues), so the GPUs rank 0 now drives carry no
+        # idle queues of other contexts.  The other ranks wait on the host
+        # (a gloo group), so no RCCL barrier kernel spins on those GPUs either.
+        ctx.close()
         wait_group = None
         if dist is not None:
             try:
