@@ -36,7 +36,10 @@ that answer against the fixture pieces tiling the rank's shard
 exits 1 after the line is printed.  `build_id` / `build_matches_tree` tie the
 measured library to the sources beside this file.
 single_process (multi-GPU runs): configs[3] once more through ONE process
-driving every GPU (SURVEY §8(e)'s process model), after every timed region.
+driving every GPU (SURVEY §8(e)'s process model), after every timed region:
+two fresh child processes with hard timeouts, one merging the 16-B shard
+results on the host, one with the in-library RCCL all-gather; a child's
+hang or abort is an entry of the line, never the loss of it.
 cpu_baseline: the reference miner fleet restated on the host -- one thread
 per core of this process's CPU share (<= 16), each a sequential miner over
 its own chunk, running the C restatement of the reference loop
@@ -147,15 +150,20 @@ def shard_check(msg: bytes, lo, hi, res):
     return None
 
 
+SP_TIMEOUT_S = 180  # per single-process child (configs[3] on one GPU opened twice: ~60 s)
+
+
 def single_process_cfg4(devices, rccl: bool):
     """configs[3] ([0, 2^40) of "bradfitz") through ONE process driving every
     device in `devices` -- SURVEY §8(e)'s own process model (one hm_open over
     the device list, hm_partition shards, 16-B results merged on the host, or
     with the in-library RCCL all-gather when `rccl`).  Timed once after a
     small untimed warm-up scan; checked against full_size.json's whole-range
-    answer.  Never raises: a failure is reported in the returned dict."""
+    answer.  Runs in a child process (run_single_process).  Never raises: a
+    failure is reported in the returned dict."""
     from distributed_bitcoinminer_amd import _lib
     m, hi = WORKLOADS["cfg4"][0], (1 << 40) - 1
+    merge_req = "rccl" if rccl else "host"
     try:
         with _lib.Context(devices) as c:
             if rccl:
@@ -166,12 +174,11 @@ def single_process_cfg4(devices, rccl: bool):
             el = time.perf_counter() - t
             st = c.stats()
     except Exception as e:  # reported, never fatal to the bench line
-        return {"devices": list(devices), "error": f"{type(e).__name__}: {e}"}
+        return {"devices": list(devices), "merge_requested": merge_req,
+                "error": f"{type(e).__name__}: {e}"}
     merge = {_lib.HM_MERGE_NONE: "none", _lib.HM_MERGE_HOST: "host",
              _lib.HM_MERGE_RCCL: "RCCL all-gather"}.get(st["merge"], str(st["merge"]))
-    return {"workload": "cfg4 in one process: hm_open over every GPU, [0, 2^40) as "
-                        "hm_partition shards, 16-B results merged (SURVEY 8(e))",
-            "devices": list(devices), "merge": merge,
+    return {"devices": list(devices), "merge_requested": merge_req, "merge": merge,
             "value": round((hi + 1) / el / 1e9, 3), "unit": "GH/s", "wall_ms": round(el * 1e3, 3),
             # kernel_ms sums the devices' busy time: nonces / it = the mean
             # per-device kernel rate
@@ -180,6 +187,106 @@ def single_process_cfg4(devices, rccl: bool):
             "enqueue_ms": round(st["enqueue_ms"], 3), "mid_call_syncs": st["mid_call_syncs"],
             "result": {"hash": res[0], "nonce": res[1]},
             "result_vs_oracle": fixture_check(m, 0, hi, res)}
+
+
+def _sp_child_main(merge: str, devices: str) -> None:
+    """Entry of a single-process child (`bench.py --sp-child host|rccl
+    --sp-devices 0,1,...`): one JSON object on stdout, exit status 0 unless
+    the interpreter itself dies.  No torch import: the child holds only its
+    hipminer context on the GPUs."""
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)  # RCCL's banner and the like go to stderr
+    out = single_process_cfg4([int(x) for x in devices.split(",") if x != ""], merge == "rccl")
+    os.write(json_fd, (json.dumps(out) + "\n").encode())
+
+
+def _run_child(cmd, timeout: float) -> dict:
+    """Run one single-process child in its own session; its last stdout line
+    is its JSON result.  A timeout kills the child's process group (by the
+    PID this function started), an abnormal exit or unreadable output is an
+    `error` entry: never an exception."""
+    import signal
+    import subprocess
+    t0 = time.perf_counter()
+    try:
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                             start_new_session=True, cwd=ROOT)
+    except OSError as e:
+        return {"error": f"could not start: {e}"}
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        try:
+            p.communicate(timeout=15)
+        except subprocess.TimeoutExpired:
+            pass
+        return {"timeout": timeout, "error": f"no result within {timeout} s (child killed)"}
+    elapsed = round(time.perf_counter() - t0, 3)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"child exit status {p.returncode}", "child_s": elapsed,
+                "stderr_tail": err[-600:]}
+    try:
+        res = json.loads(lines[-1])
+    except ValueError:
+        return {"error": "unreadable child output", "child_s": elapsed, "stdout_tail": out[-600:]}
+    res["child_s"] = elapsed
+    return res
+
+
+def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_cmd=None) -> dict:
+    """configs[3] through SURVEY §8(e)'s single-process model, measured by
+    rank 0 after every timed region of a multi-GPU line: one hipminer context
+    over every GPU in `devices`, twice, each in a FRESH CHILD PROCESS with a
+    hard timeout -- `host` merges the 16-B shard results on the host, `rccl`
+    with the in-library RCCL all-gather (ncclCommInitAll over the distinct
+    ordinals of `devices`, grouped ncclAllGather, device-side fold).  A hang,
+    abort or wrong answer in a child becomes an entry of this dict; the bench
+    line is printed either way.  `processes_per_gpu` counts the processes
+    that hold a context on each GPU while a child runs: every rank's own
+    process (its torch context and communicator on its GPU, rank_gpus[r])
+    plus the child.  child_cmd(merge, devices) -> argv is a test hook."""
+    rccl_devs = sorted(set(devices))
+    if child_cmd is None:
+        def child_cmd(merge, devs):
+            return [sys.executable, os.path.abspath(__file__), "--sp-child", merge,
+                    "--sp-devices", ",".join(str(d) for d in devs)]
+    per_gpu = {}
+    for d in devices:
+        per_gpu[d] = 1  # the child
+    for g in rank_gpus:  # each rank's own process on its GPU
+        if g in per_gpu:
+            per_gpu[g] += 1
+    out = {"workload": "cfg4 in one process: hm_open over every GPU, [0, 2^40) as "
+                       "hm_partition shards, 16-B results merged (SURVEY 8(e)); one fresh "
+                       "child process per merge, each with a hard timeout",
+           "devices": list(devices), "timeout_s": timeout,
+           "processes_per_gpu": {str(k): v for k, v in sorted(per_gpu.items())}}
+    for merge, devs in (("host", list(devices)), ("rccl", rccl_devs)):
+        res = _run_child(child_cmd(merge, devs), timeout)
+        res.setdefault("devices", devs)
+        out[merge] = res
+    return out
+
+
+def wrong_answers(line) -> list:
+    """Checks of a bench line whose answer differs from its oracle fixture:
+    the whole-job answers, the per-rank answers and the single-process
+    children's answers.  A child's error or timeout is reported in the line
+    but is not a wrong answer (the run's exit status stays 0)."""
+    secondary = line.get("workloads", {})
+    checks = [line["result_vs_oracle"], *(w["result_vs_oracle"] for w in secondary.values())]
+    sp = line.get("single_process") or {}
+    checks += [(sp.get(m) or {}).get("result_vs_oracle") for m in ("host", "rccl")]
+    wrong = [c for c in checks if c is not None and c["match"] is False]
+    wrong += [n for n, rk in [("primary", line["ranks"])] +
+              [(k, w["ranks"]) for k, w in secondary.items()] if all_match(rk) is False]
+    return wrong
 
 
 def all_match(ranks):
@@ -617,23 +724,30 @@ def main():
                 "roofline": roofline(st2, m2, lo2, hi2) if lo2 is not None else None}
 
     # configs[3] once more through SURVEY §8(e)'s single-process model, on a
-    # multi-GPU run (rank 0 drives every GPU while the other ranks wait at the
-    # barrier, after every timed region above).  HM_BENCH_SP_DEVICES (e.g.
-    # "0,0") runs it on a 1-GPU box too; HM_BENCH_SP_RCCL=1 merges with RCCL.
+    # multi-GPU run: rank 0 starts two child processes in turn (host merge,
+    # RCCL merge), each driving every GPU through one hipminer context under
+    # a hard timeout, while the other ranks wait on the host; after every
+    # timed region above.  HM_BENCH_SP_DEVICES (e.g. "0,0") runs it on a 1-GPU
+    # box too (the RCCL child then gets the distinct ordinals, "0"); "off"
+    # disables it.
     sp_env = os.environ.get("HM_BENCH_SP_DEVICES")
-    sp_devices = [int(x) for x in sp_env.split(",")] if sp_env else \
+    sp_devices = None if sp_env == "off" else \
+        [int(x) for x in sp_env.split(",")] if sp_env else \
         (list(range(world)) if world > 1 and backend == "nccl" else None)
     single = None
     if sp_devices and "cfg4" in names:
         # every rank's own context is done: closing it releases its HIP
-        # streams (hardware queues), so the GPUs rank 0 now drives carry no
-        # idle queues of other contexts.  The other ranks wait on the host
-        # (a gloo group), so no RCCL barrier kernel spins on those GPUs either.
+        # streams (hardware queues), so the GPUs the children drive carry no
+        # idle queues of this process's hipminer context.  The other ranks
+        # wait on the host (a gloo group with a timeout), so no RCCL barrier
+        # kernel spins on those GPUs either.
         ctx.close()
         wait_group = None
         if dist is not None:
             try:
-                wait_group = dist.new_group(backend="gloo")
+                import datetime
+                wait_group = dist.new_group(backend="gloo",
+                                            timeout=datetime.timedelta(seconds=4 * SP_TIMEOUT_S))
             except Exception:  # no gloo: the default (device) barrier
                 wait_group = None
         barrier()
@@ -642,7 +756,8 @@ def main():
             if max(sp_devices) >= seen:
                 single = {"devices": sp_devices, "skipped": f"rank 0 sees {seen} GPU(s)"}
             else:
-                single = single_process_cfg4(sp_devices, os.environ.get("HM_BENCH_SP_RCCL") == "1")
+                single = run_single_process(sp_devices,
+                                            list(range(world)) if backend == "nccl" else [0] * world)
         if wait_group is not None:
             dist.barrier(group=wait_group)
         barrier()
@@ -686,11 +801,7 @@ def main():
         os.write(json_fd, (json.dumps(line) + "\n").encode())
         # a wrong answer fails the run (after the line is out, so the
         # mismatching rank and device are on record)
-        checks = [line["result_vs_oracle"], *(w["result_vs_oracle"] for w in secondary.values()),
-                  (single or {}).get("result_vs_oracle")]
-        wrong = [c for c in checks if c is not None and c["match"] is False]
-        wrong += [n for n, rk in [("primary", ranks)] + [(k, w["ranks"]) for k, w in secondary.items()]
-                  if all_match(rk) is False]
+        wrong = wrong_answers(line)
         if wrong:
             print(f"bench: answers differ from the oracle fixtures: {wrong}", file=sys.stderr)
             exit_code = 1
@@ -702,4 +813,11 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--sp-child" in sys.argv:  # a single-process child (run_single_process)
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--sp-child", choices=("host", "rccl"), required=True)
+        ap.add_argument("--sp-devices", required=True)
+        a = ap.parse_args()
+        _sp_child_main(a.sp_child, a.sp_devices)
+    else:
+        main()

@@ -1,8 +1,9 @@
 """ctypes binding of libhipminer.so (include/hipminer.h).
 
 The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C
-distributed_bitcoinminer_amd/csrc``).  There is no fallback: if the library or
-a GPU is missing, the calls raise ``HipMinerError``.
+distributed_bitcoinminer_amd/csrc``).  There is no silent fallback: if the
+library or a GPU is missing, the calls raise ``HipMinerError``; ``scan_cpu``
+(hm_scan_cpu) is the host scan a caller may pick explicitly.
 """
 from __future__ import annotations
 
@@ -27,6 +28,7 @@ HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
 HM_OPT_TABLE_DIGITS = 7
 HM_OPT_TABLE_ROWS_CAP = 8
+HM_OPT_TEST_MID_SYNC = 9
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
@@ -118,6 +120,9 @@ def load() -> ctypes.CDLL:
         lib.hm_partition.restype = ctypes.c_int
         lib.hm_partition.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+        lib.hm_scan_cpu.restype = ctypes.c_int
+        lib.hm_scan_cpu.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                    ctypes.c_int, ctypes.POINTER(hm_result)]
         lib.hm_debug_plan.restype = ctypes.c_int
         lib.hm_debug_plan.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -224,6 +229,18 @@ def host_hash(msg, nonce: int) -> int:
     """hm_hash: bitcoin.Hash on the host (hash.go:13-17)."""
     m = as_bytes(msg)
     return int(load().hm_hash(m, len(m), nonce))
+
+
+def scan_cpu(msg, lo: int, hi: int, threads: int = 0) -> tuple[int, int]:
+    """hm_scan_cpu (ABI 1.7): the same scan as Context.scan on the host's
+    cores, for callers whose GPU is missing or failed; never
+    used by Context."""
+    m = as_bytes(msg)
+    out = hm_result()
+    rc = load().hm_scan_cpu(m, len(m), lo, hi, threads, ctypes.byref(out))
+    if rc != HM_OK:
+        raise HipMinerError(rc, "hm_scan_cpu")
+    return int(out.hash), int(out.nonce)
 
 
 def partition(msg, lo: int, hi: int, n: int) -> list:

@@ -85,7 +85,7 @@ struct Device {
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
     uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
-    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed at hm_close
+    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed after the call's waits
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
@@ -133,6 +133,7 @@ struct hm_ctx {
     int streams = kStreams;  // HM_OPT_STREAMS (tail filling by default)
     int table_digits = 0;    // HM_OPT_TABLE_DIGITS (test hook; 0 = default, -1 = off)
     uint64_t table_rows_cap = 0;  // HM_OPT_TABLE_ROWS_CAP (test hook; 0 = off)
+    bool test_mid_sync = false;   // HM_OPT_TEST_MID_SYNC (test hook: a host wait mid-enqueue)
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -341,9 +342,14 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
-// Host wait for stream st.  Counted in hm_stats.mid_call_syncs when the call
-// is still enqueuing work (on this or a later device): such a wait would hold
-// back every launch after it.
+// Host wait for stream st: the ONLY host wait on GPU work in a scan call
+// (the result readback; device_free at hm_close is outside any call).
+// Counted in hm_stats.mid_call_syncs when the call is still enqueuing work
+// (on this or a later device): such a wait would hold back every launch after
+// it.  No enqueue path calls it (HM_OPT_TEST_MID_SYNC makes one, so tests can
+// see the counter work); nothing on the enqueue path blocks on GPU work
+// otherwise: launches, event records, async memsets, hipMalloc of a grown
+// table (no wait on queued work).
 int host_wait(hm_ctx* ctx, hipStream_t st) {
     if (ctx->enqueuing) ++ctx->mid_syncs;
     HIPCHK(hipStreamSynchronize(st));
@@ -352,12 +358,12 @@ int host_wait(hm_ctx* ctx, hipStream_t st) {
 
 // Make stream si's K+W table hold `rows` rows.  Grown once to the largest
 // table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of
-// >= 5 digits).  Work queued earlier on any stream may still read the old
-// table, and hipFree would wait for the whole device (other contexts' work
-// on it included), so the old table is retired, not freed: the host never
-// blocks, mid-enqueue or after.  Retired tables are freed at hm_close.  Rows
-// are powers of ten and only grow, so a stream's retired tables hold less
-// than 1/9 of its current one (at most 0.28 GB beside a 10^7-row table).
+// >= 5 digits).  Work queued earlier on the stream may still read the old
+// table, and hipFree would wait for the device, so mid-enqueue the old
+// table is only retired; free_retired releases it at the end of the call,
+// once the host has waited for all of the call's work.  Peak device memory
+// during a growing call: the old and the new table (rows are powers of ten,
+// so the old one holds < 1/9 of the new one, at most 0.28 GB).
 // Returns HM_ERR_NOMEM (with HIP's error state cleared, the old table kept)
 // when the device cannot hold the table, or the HM_OPT_TABLE_ROWS_CAP test
 // hook refuses it; the caller then plans smaller tables.
@@ -373,6 +379,19 @@ int kw_table_rows(hm_ctx* ctx, Device& dv, int si, uint64_t rows) {
     dv.kwt[si] = t;
     dv.kwt_rows[si] = rows;
     ++ctx->table_grows;
+    return HM_OK;
+}
+
+// Free the K+W tables retired by kw_table_rows during the call.  Called after
+// the host has waited for every device's stream 0, which joins all of the
+// device's streams: no queued work can still read them.
+int free_retired(hm_ctx* ctx) {
+    for (auto& dv : ctx->devs) {
+        if (dv.retired.empty()) continue;
+        HIPCHK(hipSetDevice(dv.ordinal));
+        for (uint32_t* t : dv.retired) HIPCHK(hipFree(t));
+        dv.retired.clear();
+    }
     return HM_OK;
 }
 
@@ -624,6 +643,10 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
     HIPCHK(hipEventRecord(dv.join[0], s0));
     for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
+    if (ctx->test_mid_sync) {  // HM_OPT_TEST_MID_SYNC: a host wait mid-enqueue, counted
+        int rc = host_wait(ctx, s0);
+        if (rc) return rc;
+    }
     // streams == 1: every segment in order on stream 0, so kernels never
     // overlap and per-kernel timings match rocprofv3 exactly.  streams > 1:
     // the segments run by the request's dominant kernel instantiation (most
@@ -800,7 +823,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
             if (rc) return rc;
         }
         for (int r = 0; r < nreq; ++r) outs[r] = d0.host_out[r];
-        return HM_OK;
+        return free_retired(ctx);
     }
     ctx->merge = ndev > 1 ? HM_MERGE_HOST : HM_MERGE_NONE;
     for (auto& dv : ctx->devs) {
@@ -817,7 +840,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
             if (lex_less(dv.host_out[r].hash, dv.host_out[r].nonce, outs[r].hash, outs[r].nonce))
                 outs[r] = dv.host_out[r];
     }
-    return HM_OK;
+    return free_retired(ctx);
 }
 
 int open_devices(const int* devices, int ndev, hm_ctx** out);
@@ -834,8 +857,9 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
 // 1.1: hm_scan_many, hm_stats.dom_*; 1.2: hm_partition; 1.3: hm_scan_checked;
 // 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count;
 // 1.5: hm_scan_stats_sized, HM_OPT_MERGE_RCCL refused up front for repeated ordinals;
-// 1.6: hm_build_id, hm_stats.enqueue_ms / mid_call_syncs / table_grows, HM_OPT_TABLE_ROWS_CAP
-int hm_version(void) { return (1 << 16) | 6; }
+// 1.6: hm_build_id, hm_stats.enqueue_ms / mid_call_syncs / table_grows, HM_OPT_TABLE_ROWS_CAP;
+// 1.7: hm_scan_cpu, hm_scan_stats frozen at HM_STATS_SIZE_1_4 bytes
+int hm_version(void) { return (1 << 16) | 7; }
 
 // The digest of the sources this library was built from (build_id.py), kept
 // in the binary behind a tag so tools can read it without loading the library.
@@ -945,6 +969,9 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
         case HM_OPT_TABLE_ROWS_CAP:
             if (value < 0) return HM_ERR_INVALID;
             ctx->table_rows_cap = (uint64_t)value;
+            return HM_OK;
+        case HM_OPT_TEST_MID_SYNC:
+            ctx->test_mid_sync = value != 0;
             return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;
@@ -1096,7 +1123,9 @@ int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, ui
 
 
 int hm_scan_stats(const hm_ctx* ctx, hm_stats* out) {
-    return hm_scan_stats_sized(ctx, out, sizeof(hm_stats));
+    // frozen at the 1.4/1.5 size (include/hipminer.h): newer fields only
+    // through hm_scan_stats_sized
+    return hm_scan_stats_sized(ctx, out, HM_STATS_SIZE_1_4);
 }
 
 int hm_scan_stats_sized(const hm_ctx* ctx, hm_stats* out, size_t size) {

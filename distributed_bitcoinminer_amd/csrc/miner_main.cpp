@@ -6,11 +6,17 @@
 // NewResult(hash, nonce) (evalRoutine, :36-68; Result write :60-62) -- but
 // over the native LSP client (lsp_client.cpp) and with the scan (:46-59,
 // init :48-49) on the GPU through hm_scan.  The `upper := Upper+1` uint64
-// wrap (:52) is kept.  A GPU failure ends the process (no CPU fallback), like
-// an LSP error ends the reference miner; the server then reassigns the chunk
-// (server.go:326-376).
+// wrap (:52) is kept.
 //
-// Env: HIPMINER_DEVICES=0,1 (default: all visible), HM_LSP_* (lsp_client.hpp).
+// Liveness: the reference miner answers every Request.  When
+// hm_open finds no usable GPU, or an hm_scan fails, this miner says so on
+// stderr and scans on the host instead (hm_scan_cpu, bit-identical), from
+// then on: a Result is still written, so the unchanged server never has to
+// wait out its 10-s drop timer (params.go:8-13) and reassign the chunk
+// (server.go:326-376).  Only a bad HIPMINER_DEVICES list ends the process.
+//
+// Env: HIPMINER_DEVICES=0,1 (default: all visible), HM_CPU_THREADS (host
+// scan threads, default every hardware thread), HM_LSP_* (lsp_client.hpp).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,15 +66,22 @@ int main(int argc, char** argv) {
     std::vector<int> ds = devices_from_env();
     hm_ctx* gpu = nullptr;
     int rc = hm_open(ds.empty() ? nullptr : ds.data(), (int)ds.size(), &gpu);
-    if (rc != HM_OK) {
-        fprintf(stderr, "hm_miner: GPU init failed: %s\n", hm_strerror(rc));
+    if (rc == HM_ERR_INVALID) {
+        fprintf(stderr, "hm_miner: bad HIPMINER_DEVICES: %s\n", hm_strerror(rc));
         return 1;
+    }
+    const char* th = getenv("HM_CPU_THREADS");
+    const int cpu_threads = th ? atoi(th) : 0;
+    if (rc != HM_OK) {
+        gpu = nullptr;
+        fprintf(stderr, "hm_miner: NO GPU (%s): every Request is scanned on the host "
+                        "(hm_scan_cpu), orders of magnitude slower\n", hm_strerror(rc));
     }
     std::string err;
     auto conn = hm::LspClient::connect(argv[1], hm::LspParams::from_env(), &err);
     if (!conn) {
         printf("Failed to join with server: %s\n", err.c_str());
-        hm_close(gpu);
+        if (gpu) hm_close(gpu);
         return 0;
     }
     BitcoinMsg join;  // NewJoin (message.go:47-49)
@@ -83,13 +96,26 @@ int main(int argc, char** argv) {
             res.nonce = 0;  // miner.go:48-49
             const uint64_t end = req.upper + 1;  // miner.go:52, wraps
             if (req.lower < end) {
+                const uint8_t* msg = reinterpret_cast<const uint8_t*>(req.data.data());
                 hm_result out;
-                rc = hm_scan(gpu, reinterpret_cast<const uint8_t*>(req.data.data()), req.data.size(),
-                             req.lower, end - 1, &out);
+                rc = HM_ERR_NO_DEVICE;
+                if (gpu) {
+                    rc = hm_scan(gpu, msg, req.data.size(), req.lower, end - 1, &out);
+                    if (rc != HM_OK) {
+                        fprintf(stderr, "hm_miner: GPU scan FAILED (%s): this and every later "
+                                        "Request are scanned on the host (hm_scan_cpu)\n",
+                                hm_strerror(rc));
+                        hm_close(gpu);
+                        gpu = nullptr;
+                    }
+                }
                 if (rc != HM_OK) {
-                    fprintf(stderr, "hm_miner: scan failed: %s\n", hm_strerror(rc));
-                    status = 2;
-                    break;
+                    rc = hm_scan_cpu(msg, req.data.size(), req.lower, end - 1, cpu_threads, &out);
+                    if (rc != HM_OK) {
+                        fprintf(stderr, "hm_miner: host scan failed: %s\n", hm_strerror(rc));
+                        status = 2;
+                        break;
+                    }
                 }
                 res.hash = out.hash;
                 res.nonce = out.nonce;
@@ -99,6 +125,6 @@ int main(int argc, char** argv) {
     }
     if (status == 0) conn->close();
     conn.reset();
-    hm_close(gpu);
+    if (gpu) hm_close(gpu);
     return status;
 }

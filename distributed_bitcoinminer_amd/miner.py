@@ -9,10 +9,10 @@ uint64 add, so ``Upper == 2^64-1`` scans nothing and yields
 ``(MaxUint64, 0)``; that quirk (SURVEY A-inv-5) is reproduced here, in the
 caller, exactly as the Go shim in go/src/hipminer does it.
 
-There is no CPU fallback: if the GPU path fails, ``HipMinerError`` propagates
-and the miner process ends, as the reference miner does on an LSP error
-(miner.go:40-43, 63-66); the unchanged server then reassigns its chunk
-(server.go:326-376).
+This adapter is GPU-only: if the GPU path fails, ``HipMinerError``
+propagates.  The miner processes (hm_miner, Go gpuminer) instead fall back to
+the host scan hm_scan_cpu (``_lib.scan_cpu``) so that a Result is always
+written; ``eval_range`` gives the range either one scans.
 """
 from __future__ import annotations
 

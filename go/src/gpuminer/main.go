@@ -3,7 +3,8 @@
 // cmu440/bitcoin/miner (Join, then Request -> Result), but the scan runs in
 // libhipminer.so through package hipminer.
 //
-// Usage: gpuminer <host:port>     (HIPMINER_DEVICES=0,1,... selects GPUs)
+// Usage: gpuminer <host:port>     (HIPMINER_DEVICES=0,1,... selects GPUs;
+// HM_CPU_THREADS sizes the host scan used when no GPU works)
 // Build (GOPATH mode: the reference's p1/ and this repo's go/ as GOPATH entries):
 //
 //	GO111MODULE=off GOPATH=<reference>/p1:<repo>/go go build gpuminer
@@ -11,6 +12,7 @@ package main
 
 import (
 	"encoding/json"
+	"errors"
 	"fmt"
 	"os"
 	"strconv"
@@ -22,6 +24,8 @@ import (
 	"hipminer"
 )
 
+var errNoGPU = errors.New("no GPU")
+
 func devicesFromEnv() []int {
 	var ds []int
 	for _, f := range strings.Split(os.Getenv("HIPMINER_DEVICES"), ",") {
@@ -32,9 +36,11 @@ func devicesFromEnv() []int {
 	return ds
 }
 
-// serve answers Requests until the connection fails; a GPU failure ends the
-// process (no CPU fallback): the server then reassigns the chunk.
-func serve(conn lsp.Client, gpu *hipminer.Miner) error {
+// serve answers Requests until the connection fails.  gpu == nil, or a
+// failed GPU scan, sends every (later) Request to the host scan, loudly: a
+// Result is always written, as the reference miner writes one
+// (miner.go:60-62; SURVEY §8(b)).
+func serve(conn lsp.Client, gpu *hipminer.Miner, cpuThreads int) error {
 	for {
 		payload, err := conn.Read()
 		if err != nil {
@@ -42,9 +48,20 @@ func serve(conn lsp.Client, gpu *hipminer.Miner) error {
 		}
 		var req bitcoin.Message
 		_ = json.Unmarshal(payload, &req) // the reference ignores decode errors
-		h, n, err := gpu.EvalRequest(req.Data, req.Lower, req.Upper)
+		var h, n uint64
+		err = errNoGPU
+		if gpu != nil {
+			if h, n, err = gpu.EvalRequest(req.Data, req.Lower, req.Upper); err != nil {
+				fmt.Fprintln(os.Stderr, "gpuminer: GPU scan FAILED:", err,
+					"- this and every later Request are scanned on the host (hm_scan_cpu)")
+				gpu.Close()
+				gpu = nil
+			}
+		}
 		if err != nil {
-			return err
+			if h, n, err = hipminer.EvalRequestCPU(req.Data, req.Lower, req.Upper, cpuThreads); err != nil {
+				return err
+			}
 		}
 		out, _ := json.Marshal(bitcoin.NewResult(h, n))
 		if err := conn.Write(out); err != nil {
@@ -59,11 +76,16 @@ func main() {
 		return
 	}
 	gpu, err := hipminer.Open(devicesFromEnv()...)
-	if err != nil {
-		fmt.Println("GPU init failed:", err)
+	if e, ok := err.(hipminer.Error); ok && e.Code == hipminer.ErrInvalid {
+		fmt.Println("bad HIPMINER_DEVICES:", err)
 		return
 	}
-	defer gpu.Close()
+	if err != nil {
+		gpu = nil
+		fmt.Fprintln(os.Stderr, "gpuminer: NO GPU:", err,
+			"- every Request is scanned on the host (hm_scan_cpu), orders of magnitude slower")
+	}
+	cpuThreads, _ := strconv.Atoi(os.Getenv("HM_CPU_THREADS"))
 	conn, err := lsp.NewClient(os.Args[1], lsp.NewParams())
 	if err != nil {
 		fmt.Println("Failed to join with server:", err)
@@ -74,7 +96,11 @@ func main() {
 	if err := conn.Write(join); err != nil {
 		return
 	}
-	if err := serve(conn, gpu); err != nil {
+	err = serve(conn, gpu, cpuThreads)
+	if gpu != nil {
+		gpu.Close()
+	}
+	if err != nil {
 		fmt.Fprintln(os.Stderr, "gpuminer:", err)
 	}
 }

@@ -36,6 +36,12 @@ func cbytes(s string) *C.uint8_t {
 	return (*C.uint8_t)(C.CBytes([]byte(s)))
 }
 
+// Return codes of include/hipminer.h that callers branch on.
+const (
+	ErrInvalid  = int(C.HM_ERR_INVALID)
+	ErrNoDevice = int(C.HM_ERR_NO_DEVICE)
+)
+
 // Error carries an hm_* return code.
 type Error struct{ Code int }
 
@@ -142,6 +148,31 @@ func (m *Miner) EvalRequest(data string, lower, upper uint64) (hash, nonce uint6
 		return maxUint64, 0, nil
 	}
 	return m.ScanInclusive(data, lower, end-1)
+}
+
+// ScanCPU is hm_scan_cpu: the same scan as ScanInclusive, bit-identical, on
+// the host's cores (threads <= 0: every hardware thread).  For a miner whose
+// GPU is missing or failed, so that a Result is still written (SURVEY
+// §8(b)); orders of magnitude slower than the GPU.
+func ScanCPU(data string, lo, hi uint64, threads int) (hash, nonce uint64, err error) {
+	var out C.hm_result
+	p := cbytes(data)
+	defer C.free(unsafe.Pointer(p))
+	rc := C.hm_scan_cpu(p, C.size_t(len(data)), C.uint64_t(lo), C.uint64_t(hi), C.int(threads), &out)
+	if rc != 0 {
+		return 0, 0, Error{int(rc)}
+	}
+	return uint64(out.hash), uint64(out.nonce), nil
+}
+
+// EvalRequestCPU is EvalRequest on the host (ScanCPU), with the same
+// `upper := Upper + 1` wrap and initial (MaxUint64, 0).
+func EvalRequestCPU(data string, lower, upper uint64, threads int) (hash, nonce uint64, err error) {
+	end := upper + 1 // wraps exactly like miner.go:52
+	if !(lower < end) {
+		return maxUint64, 0, nil
+	}
+	return ScanCPU(data, lower, end-1, threads)
 }
 
 // Close releases the context.

@@ -37,8 +37,10 @@
  * the context's lifetime, as with any C handle).
  *
  * Errors: 0 = HM_OK; negative codes below; hm_strerror() describes them.
- * Nothing aborts the process and there is no CPU fallback: a failed GPU scan
- * is reported, never silently replaced.
+ * Nothing aborts the process, and a failed GPU scan is reported, never
+ * silently replaced.  hm_scan_cpu (ABI 1.7) is the host scan a caller may
+ * choose when hm_open or hm_scan fails, so that a Result is still written
+ * (SURVEY §8(b)); the GPU entry points never call it.
  */
 #ifndef HIPMINER_H
 #define HIPMINER_H
@@ -104,8 +106,10 @@ typedef struct hm_stats {
                                 host waits on any, so devices overlap)          */
     int32_t table_grows;     /* chained K+W tables enlarged by the call; an old
                                 table may still be read by queued work, so it
-                                is kept (< 1/9 of the new one) until hm_close:
-                                growth never waits on the device (ABI 1.6)      */
+                                is kept (< 1/9 of the new one) until the call
+                                has waited for its work and freed then (ABI
+                                1.7; 1.6 kept it until hm_close): growth never
+                                waits on the device mid-enqueue (ABI 1.6)     */
 } hm_stats;
 
 /* sizeof(hm_stats) by ABI version.  The struct only grows at its end. */
@@ -159,6 +163,10 @@ typedef struct hm_stats {
                                   falls back to smaller tables and more epochs
                                   (the HM_ERR_NOMEM path of table growth; ABI
                                   1.6)                                          */
+#define HM_OPT_TEST_MID_SYNC 9  /* test hook (0/1): the call waits on the host for
+                                  each device's first queued work while still
+                                  enqueuing, which hm_stats.mid_call_syncs must
+                                  count (ABI 1.7)                               */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */
@@ -213,16 +221,31 @@ int hm_scan_checked(hm_ctx *ctx, const uint8_t *msg, size_t len, uint64_t lo, ui
 int hm_partition(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int n,
                  uint64_t *bounds);
 
-/* Stats of the last successful hm_scan / hm_scan_many on ctx.  Writes
- * sizeof(hm_stats) of THIS header (HM_STATS_SIZE_1_6 bytes): a caller built
- * against an older header (136 or 144 bytes, ABI <= 1.5) must use
- * hm_scan_stats_sized instead, or check hm_version() >= 0x10006 first. */
+/* Stats of the last successful hm_scan / hm_scan_many on ctx: the FIRST
+ * HM_STATS_SIZE_1_4 BYTES ONLY (through dom_compressions_eff), the size the
+ * ABI 1.4/1.5 headers promised.  Frozen since ABI 1.7, so a binary built
+ * against any header from 1.4 on never gets more bytes than its struct
+ * holds (ABI 1.6 wrote 160 bytes here, past a 1.5 caller's struct).  The
+ * fields after dom_compressions_eff come only from hm_scan_stats_sized. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
 
 /* hm_scan_stats writing at most `size` bytes (pass sizeof(hm_stats) as the
  * caller compiled it; >= HM_STATS_SIZE_1_0): the prefix of the current
- * layout that fits.  ABI 1.5. */
+ * layout that fits.  ABI 1.5.  The call to use for every field. */
 int hm_scan_stats_sized(const hm_ctx *ctx, hm_stats *out, size_t size);
+
+/* The same scan as hm_scan -- lexicographic min of (Hash(msg, n), n) over
+ * the INCLUSIVE [lo, hi], seeded (UINT64_MAX, 0), bit-identical -- on the
+ * host's cores, without a GPU (ABI 1.7; SURVEY §8(b)'s liveness path).
+ * `threads` <= 0 uses every hardware thread; the range is split into that
+ * many contiguous chunks (ranges below 4096 nonces per thread use fewer).
+ * x86 SHA extensions when the CPU has them (HM_CPU_NO_SHA=1 forces portable
+ * C).  Orders of magnitude slower than hm_scan: for callers whose GPU is
+ * missing or failed (hm_miner, the Go gpuminer), so a Result is still
+ * written; never called by the GPU entry points.  `out` is written only on
+ * HM_OK. */
+int hm_scan_cpu(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int threads,
+                hm_result *out);
 
 int hm_set_option(hm_ctx *ctx, int opt, int64_t value);
 

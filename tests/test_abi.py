@@ -13,7 +13,8 @@ def test_exports_every_header_symbol():
     syms = _lib.header_symbols()
     assert set(syms) >= {"hm_hash", "hm_open", "hm_scan", "hm_scan_stats", "hm_set_option",
                          "hm_strerror", "hm_close", "hm_version", "hm_scan_checked",
-                         "hm_scan_many", "hm_partition", "hm_scan_stats_sized", "hm_build_id"}
+                         "hm_scan_many", "hm_partition", "hm_scan_stats_sized", "hm_build_id",
+                         "hm_scan_cpu"}
     for s in syms:
         assert hasattr(lib, s), s
 
@@ -26,7 +27,7 @@ def test_library_is_gfx950_code_object():
 def test_version_and_strerror():
     lib = _lib.load()
     assert lib.hm_version() >> 16 == 1
-    assert lib.hm_version() & 0xFFFF >= 6  # 1.6: hm_build_id, hm_stats.enqueue_ms ..
+    assert lib.hm_version() & 0xFFFF >= 7  # 1.7: hm_scan_cpu, hm_scan_stats frozen at 144 B
     for rc in range(0, -7, -1):
         assert _lib.strerror(rc)
     assert _lib.strerror(-99) == "unknown error"
@@ -148,3 +149,22 @@ def test_build_id_changes_with_any_source(tmp_path):
         assert bid.tree_digest(str(root)) != base, rel
         p.write_bytes(data)
     assert bid.tree_digest(str(root)) == base
+
+
+@pytest.mark.gpu
+def test_scan_stats_writes_only_the_frozen_144_bytes(ctx):
+    """ABI 1.7: hm_scan_stats writes HM_STATS_SIZE_1_4 bytes, never more, so a
+    caller built against the 1.4/1.5 header (144-byte struct) is safe; the
+    later fields come through hm_scan_stats_sized."""
+    ctx.scan(b"bradfitz", 0, 99_999)
+    lib = _lib.load()
+    buf = (ctypes.c_uint8 * 256)(*([0xA5] * 256))
+    assert lib.hm_scan_stats(ctx._h, ctypes.cast(buf, ctypes.POINTER(_lib.hm_stats))) == 0
+    assert all(b == 0xA5 for b in buf[144:]), "hm_scan_stats wrote past 144 bytes"
+    st = _lib.hm_stats.from_buffer_copy(bytes(buf[:160]))
+    full = ctx.stats()
+    assert st.nonces == full["nonces"] == 100_000
+    assert st.dom_compressions_eff == full["dom_compressions_eff"] > 0
+    buf2 = (ctypes.c_uint8 * 256)(*([0xA5] * 256))
+    assert lib.hm_scan_stats_sized(ctx._h, ctypes.cast(buf2, ctypes.POINTER(_lib.hm_stats)), 160) == 0
+    assert all(b == 0xA5 for b in buf2[160:]) and bytes(buf2[:144]) == bytes(buf[:144])

@@ -138,12 +138,67 @@ def test_all_match():
 
 
 def test_single_process_failure_is_reported_not_raised():
-    """bench.single_process_cfg4 runs after every timed region of a multi-GPU
-    line; a failure there (here: no GPU, hm_open fails) must land in the line,
-    never abort the run that prints it."""
+    """bench.single_process_cfg4 runs (in a child) after every timed region of
+    a multi-GPU line; a failure there (here: no GPU, hm_open fails) must land
+    in the line, never abort the run that prints it."""
     import torch
     if torch.cuda.is_available():
         import pytest
         pytest.skip("GPU present")
     out = bench.single_process_cfg4([0, 1], rccl=True)
     assert out["devices"] == [0, 1] and "HipMinerError" in out["error"]
+    assert out["merge_requested"] == "rccl"
+
+
+def test_single_process_children_report_failures():
+    """rank 0 runs the single-process workload as two fresh child processes
+    (host merge, RCCL merge over the distinct ordinals): here, without a GPU,
+    the real children start, fail in hm_open and report it as their entry;
+    the per-GPU process count covers every rank's process plus the child."""
+    import torch
+    if torch.cuda.is_available():
+        import pytest
+        pytest.skip("GPU present")
+    out = bench.run_single_process([0, 0], [0, 0, 0], timeout=120)
+    assert out["host"]["devices"] == [0, 0] and out["rccl"]["devices"] == [0]
+    for m in ("host", "rccl"):
+        assert "HipMinerError" in out[m]["error"], out[m]
+        assert out[m]["merge_requested"] == m and out[m]["child_s"] > 0
+    assert out["processes_per_gpu"] == {"0": 4}
+    out = bench.run_single_process([0, 1, 2, 3], [0, 1, 2, 3], timeout=120,
+                                   child_cmd=lambda m, d: ["true"])
+    assert out["processes_per_gpu"] == {str(g): 2 for g in range(4)}
+
+
+def test_single_process_child_timeout_and_crash_become_entries():
+    """A child that hangs is killed at its timeout, one that dies is an error
+    entry with its exit status: run_single_process returns either way."""
+    import sys
+    import time
+    t = time.perf_counter()
+    out = bench.run_single_process(
+        [0, 1], [0, 1], timeout=2,
+        child_cmd=lambda m, d: [sys.executable, "-c", "import time; time.sleep(60)"] if m == "rccl"
+        else [sys.executable, "-c", "import sys; sys.exit(3)"])
+    assert time.perf_counter() - t < 40
+    assert out["rccl"]["timeout"] == 2 and "killed" in out["rccl"]["error"]
+    assert "exit status 3" in out["host"]["error"]
+    ok = {"devices": [0, 1], "merge": "host", "result_vs_oracle": {"match": True}}
+    out = bench.run_single_process(
+        [0, 1], [0, 1], timeout=30,
+        child_cmd=lambda m, d: [sys.executable, "-c",
+                                "import json; print('banner'); print(json.dumps(%r))" % ok])
+    assert out["host"]["result_vs_oracle"]["match"] is True and out["host"]["child_s"] > 0
+
+
+def test_wrong_answers_ignores_child_errors():
+    """The line's exit status: a child's error or timeout is reported, not a
+    wrong answer; a child whose answer differs from the fixture is."""
+    line = {"result_vs_oracle": {"match": True}, "ranks": {"match": [True]},
+            "workloads": {"cfg4": {"result_vs_oracle": {"match": True}, "ranks": {"match": [True]}}},
+            "single_process": {"host": {"error": "x"}, "rccl": {"timeout": 5, "error": "y"}}}
+    assert bench.wrong_answers(line) == []
+    line["single_process"]["rccl"] = {"result_vs_oracle": {"match": False}}
+    assert len(bench.wrong_answers(line)) == 1
+    line["ranks"]["match"] = [True, False]
+    assert "primary" in bench.wrong_answers(line)

@@ -117,7 +117,8 @@ def test_every_c_name_is_declared_and_calls_match_arity():
     protos = _c_prototypes()
     names = set(re.findall(r"\bC\.(\w+)", src))
     assert {"hm_open", "hm_scan", "hm_scan_many", "hm_scan_checked", "hm_partition",
-            "hm_hash", "hm_close", "hm_strerror"} <= names
+            "hm_hash", "hm_close", "hm_strerror", "hm_scan_cpu", "HM_ERR_INVALID",
+            "HM_ERR_NO_DEVICE"} <= names
     for n in sorted(names - CGO_BUILTINS):
         declared = n in protos or re.search(rf"(\btypedef struct {n}\b|}} {n};|^#define {n}\b)", hdr, re.M)
         assert declared, f"C.{n} is not declared by include/hipminer.h"
@@ -160,6 +161,11 @@ int main(int argc, char **argv) {
     for (int i = 0; i < 2 * n; ++i) printf(" %llu", (unsigned long long)bounds[i]);
     printf("\n");
     if (hm_partition(p, (size_t)len, 0, 1, 0, &bounds[0]) != HM_ERR_INVALID) return 3;
+
+    /* ScanCPU(data, lo, hi, threads): the host scan a GPU-less miner uses */
+    hm_result cpu;
+    rc = hm_scan_cpu(p, (size_t)len, (uint64_t)0, (uint64_t)9999, (int)2, &cpu);
+    printf("cpu %d %llu %llu\n", rc, (unsigned long long)cpu.hash, (unsigned long long)cpu.nonce);
 
     /* Open(devices...): both forms; no GPU here -> HM_ERR_NO_DEVICE */
     hm_ctx *ctx = NULL, *all = NULL;
@@ -211,6 +217,7 @@ def test_preamble_and_call_replay_compile_link_and_run(tmp_path, golden):
     rc, *b = [int(x) for x in lines["partition"].split()]
     assert rc == 0
     assert b == [x for pair in _lib.partition(b"bradfitz", 0, (1 << 40) - 1, 8) for x in pair]
+    assert [int(x) for x in lines["cpu"].split()] == [0, 1419516646206828, 9898]
     rc0, rc1, why = lines["open"].split(" ", 2)
     import torch
     if not torch.cuda.is_available():

@@ -121,28 +121,39 @@ def test_bench_torchrun_rccl_all_visible_gpus():
     _per_rank(c4["ranks"], n, list(range(n)))
     assert len({d["pci_bus_id"] for d in line["ranks"]["device"]}) == n
     assert line["all_ranks_match"] is True and c4["all_ranks_match"] is True
-    # configs[3] again through one process driving all n GPUs
+    # configs[3] again through one process driving all n GPUs: two children,
+    # host merge and the in-library RCCL all-gather over distinct ordinals
     sp = line["single_process"]
-    assert sp["devices"] == list(range(n)) and sp["merge"] == "host", sp
-    assert sp["result_vs_oracle"]["match"] is True and sp["mid_call_syncs"] == 0, sp
+    assert sp["processes_per_gpu"] == {str(g): 2 for g in range(n)}, sp
+    for m, merge in (("host", "host"), ("rccl", "RCCL all-gather")):
+        e = sp[m]
+        assert e["devices"] == list(range(n)) and e["merge"] == merge, e
+        assert e["result_vs_oracle"]["match"] is True and e["mid_call_syncs"] == 0, e
 
 
 def test_bench_single_process_workload_on_one_gpu():
     """bench.py's single-process configs[3] measurement (the line's
     `single_process`, taken on multi-GPU runs) exercised on a 1-GPU box:
-    HM_BENCH_SP_DEVICES=0,0 opens GPU 0 twice, so the hm_partition shards,
-    the per-device enqueue and the host merge of a 2-device context run on
-    [0, 2^40), and the answer equals full_size.json's.  Launched as the
+    HM_BENCH_SP_DEVICES=0,0 opens GPU 0 twice in the host-merge child, so the
+    hm_partition shards, the per-device enqueue and the host merge of a
+    2-device context run on [0, 2^40); the RCCL child gets the distinct
+    ordinal 0 (a 1-rank communicator, ncclCommInitAll + ncclAllGather +
+    device fold).  Both answers equal full_size.json's.  Launched as the
     driver launches bench.py (torch.distributed.run, RCCL process group at
     world size 1 via HM_BENCH_FORCE_DIST), so the host-side (gloo) wait group
     the other ranks park on is created and used too."""
     line = _torchrun(1, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
                          "--no-cpu-baseline"],
-                     {"HM_BENCH_FORCE_DIST": "1", "HM_BENCH_SP_DEVICES": "0,0"}, timeout=400)
+                     {"HM_BENCH_FORCE_DIST": "1", "HM_BENCH_SP_DEVICES": "0,0"}, timeout=500)
     assert line["config"]["merge"] == "RCCL all-gather"
     sp = line["single_process"]
-    assert "error" not in sp and "skipped" not in sp, sp
-    assert sp["devices"] == [0, 0] and sp["merge"] == "host"
-    assert sp["result_vs_oracle"]["match"] is True, sp
-    assert sp["result"] == line["workloads"]["cfg4"]["result"]
-    assert sp["mid_call_syncs"] == 0 and sp["value"] > 0
+    assert "skipped" not in sp, sp
+    # GPU 0 holds the rank's own process and the child
+    assert sp["processes_per_gpu"] == {"0": 2}, sp
+    for m, devs, merge in (("host", [0, 0], "host"), ("rccl", [0], "RCCL all-gather")):
+        e = sp[m]  # each measured in a fresh child process
+        assert "error" not in e, e
+        assert e["devices"] == devs and e["merge"] == merge, e
+        assert e["result_vs_oracle"]["match"] is True, e
+        assert e["result"] == line["workloads"]["cfg4"]["result"]
+        assert e["mid_call_syncs"] == 0 and e["value"] > 0 and e["child_s"] > 0

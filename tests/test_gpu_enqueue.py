@@ -1,9 +1,10 @@
 """The host never waits on the GPU while a call is still enqueuing (ABI 1.6).
 
 Chained f >= 5 segments grow their stream's K+W table (10^5 .. 10^7 rows).
-Work queued earlier may still read the old table, so it is retired (kept
-until hm_close, api.cpp kw_table_rows) instead of freed, which would drain
-the device mid-enqueue: every device of a
+Work queued earlier may still read the old table, so it is retired (api.cpp
+kw_table_rows; freed at the end of the call since ABI 1.7, after the host
+has waited for the call's work) instead of freed, which would drain the
+device mid-enqueue: every device of a
 context gets its work before the host waits on any of it (one
 context drives all of a miner's GPUs).  hm_stats counts the waits issued while
 enqueuing (mid_call_syncs), the tables grown (table_grows) and the host time
@@ -104,3 +105,20 @@ def test_table_rows_cap_falls_back_to_epochs(oracle_mod, cap, req, f):
         st = c.stats()
         assert st["table_grows"] >= 1 and st["dom_launches"] < n_capped, st
     assert f in _chained_f(m, lo, hi)
+
+
+def test_mid_call_sync_counter_counts(oracle_mod):
+    """hm_stats.mid_call_syncs is live: the test hook HM_OPT_TEST_MID_SYNC puts
+    a host wait into each device's enqueue, and the counter sees one per
+    device (0 without the hook); the answers do not change."""
+    m, lo, hi = b"bradfitz", 10**9, 10**9 + 50_000_000
+    exp = oracle_mod.fast_scan_sum(m, lo, hi, threads=THREADS)[0]
+    with _lib.Context([0, 0]) as c:
+        assert c.scan(m, lo, hi) == exp
+        assert c.stats()["mid_call_syncs"] == 0
+        c.set_option(_lib.HM_OPT_TEST_MID_SYNC, 1)
+        assert c.scan(m, lo, hi) == exp
+        assert c.stats()["mid_call_syncs"] == 2, c.stats()
+        c.set_option(_lib.HM_OPT_TEST_MID_SYNC, 0)
+        assert c.scan(m, lo, hi) == exp
+        assert c.stats()["mid_call_syncs"] == 0
