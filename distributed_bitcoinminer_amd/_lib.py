@@ -24,11 +24,13 @@ HM_ERR_NOMEM = -4
 HM_ERR_RCCL = -5
 HM_ERR_INTERNAL = -6
 
-HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED = 0, 1, 2, 3
+HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED, HM_KIND_FUSED = 0, 1, 2, 3, 4
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
 HM_OPT_TABLE_DIGITS = 7
 HM_OPT_TABLE_ROWS_CAP = 8
 HM_OPT_TEST_MID_SYNC = 9
+HM_OPT_FUSED = 10
+HM_OPT_FUSED_FLAGS = 11
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 

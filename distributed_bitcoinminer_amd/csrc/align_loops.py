@@ -132,6 +132,41 @@ def hot_loop(insts, heads):
     return best
 
 
+def all_loops(insts, heads):
+    """Every innermost loop with >= MIN_LOOP instructions, in address order
+    (the fused kernel holds one hot loop per segment layout)."""
+    out = []
+    addr_index = {x[0]: i for i, x in enumerate(insts)}
+    for k in heads:
+        if k >= len(insts):
+            continue
+        head = insts[k][0]
+        ends = [(i, x[3]) for i, x in enumerate(insts)
+                if i > k and x[3] is not None and head - LATCH_BYTES <= x[3] <= head]
+        if not ends:
+            continue
+        end, target = max(ends)
+        first = addr_index[target]
+        if end - first + 1 >= MIN_LOOP:
+            out.append((first, end))
+    out = sorted(set(out))
+    # innermost loops do not overlap; keep the first of any that would
+    keep = []
+    for lp in out:
+        if not keep or lp[0] > keep[-1][1]:
+            keep.append(lp)
+    return keep
+
+
+def kernel_loops(sym, insts, heads):
+    """The loops the pass places: every hot loop of the fused kernels, the
+    single hottest loop of every other kernel."""
+    if "fused" in sym:
+        return all_loops(insts, heads)
+    lp = hot_loop(insts, heads)
+    return [lp] if lp else []
+
+
 PHASE = 4  # target start address mod 8 of 8-byte VALU instructions
 NO_NOP = False
 ALL_E64 = True  # re-encode every full-rate 4-byte VALU op of the loop
@@ -306,42 +341,41 @@ def check_blocks(before, after):
             raise SystemExit(f"block {x[0]} changed by the placement pass")
 
 
-def main():
-    global PHASE, NO_NOP, ALL_E64
-    src, dst = sys.argv[1], sys.argv[2]
-    report = "--report" in sys.argv
-    if "--phase" in sys.argv:
-        PHASE = int(sys.argv[sys.argv.index("--phase") + 1])
-    NO_NOP = "--no-nop" in sys.argv
-    ALL_E64 = "--keep-e32" not in sys.argv
-    with open(src) as f:
-        lines = f.read().split("\n")
+def place(lines, report):
+    """One placement pass over the assembly lines: returns the edited lines
+    and {kernel: number of loops placed}."""
     with tempfile.TemporaryDirectory() as td:
         obj = os.path.join(td, "in.o")
-        assemble(src, obj)
+        path = os.path.join(td, "in.s")
+        with open(path, "w") as f:
+            f.write("\n".join(lines))
+        assemble(path, obj)
         funcs = disassemble(obj)
-        where = source_insts(lines)
-        edits = {}  # line index -> replacement text
-        loops = {}
-        for sym, insts in funcs.items():
-            if sym not in where:
-                continue
-            idx = where[sym]
-            # the disassembly may list the inter-function alignment padding too
-            if len(idx) > len(insts):
-                raise SystemExit(f"{sym}: {len(idx)} source vs {len(insts)} encoded instructions")
-            loop = hot_loop(insts, inner_headers(lines, idx))
-            if loop is None:
-                continue
-            loops[sym] = loop
-            for k, (_, _, op, _) in enumerate(insts[:len(idx)]):
-                if INST.match(lines[idx[k]]).group(1) != op:
-                    raise SystemExit(f"{sym}: instruction {k} is {op} in the object, "
-                                     f"'{lines[idx[k]].strip()}' in the source")
-            lo, hi = loop
+    where = source_insts(lines)
+    edits = {}  # line index -> replacement text
+    placed = {}
+    for sym, insts in funcs.items():
+        if sym not in where:
+            continue
+        idx = where[sym]
+        # the disassembly may list the inter-function alignment padding too
+        if len(idx) > len(insts):
+            raise SystemExit(f"{sym}: {len(idx)} source vs {len(insts)} encoded instructions")
+        loops = kernel_loops(sym, insts, inner_headers(lines, idx))
+        if not loops:
+            continue
+        placed[sym] = len(loops)
+        for k, (_, _, op, _) in enumerate(insts[:len(idx)]):
+            if INST.match(lines[idx[k]]).group(1) != op:
+                raise SystemExit(f"{sym}: instruction {k} is {op} in the object, "
+                                 f"'{lines[idx[k]].strip()}' in the source")
+        shift = 0  # bytes the edits of earlier loops of this kernel add
+        for lo, hi in loops:
+            shifted = [(a + shift, sz, op, t) for a, sz, op, t in insts] if shift else insts
             text = {k: lines[idx[k]] for k in range(lo, hi + 1)}
             between = {p: lines[idx[lo + p - 1] + 1: idx[lo + p]] for p in range(1, hi - lo + 1)}
-            order, promote, nops = plan_fixes(insts, lo, hi, text, between)
+            order, promote, nops = plan_fixes(shifted, lo, hi, text, between)
+            shift += 4 * (len(promote) + len(nops))
             new = {}
             for k in range(lo, hi + 1):
                 t = text[k]
@@ -353,27 +387,64 @@ def main():
             for slot, k in zip(range(lo, hi + 1), order):
                 edits[idx[slot]] = new[k]
             if report:
-                good, n = stats(insts, lo, hi)
+                good, n = stats(shifted, lo, hi)
                 moved = sum(1 for a, b in zip(range(lo, hi + 1), order) if a != b) // 2
                 print(f"{sym[:64]:64s} loop {hi - lo + 1:5d} insts: {good:4d}/{n} 8-B VALU at "
                       f"4 mod 8 -> re-encode {len(promote)}, move {moved}, s_nop {len(nops)}")
-        with open(dst, "w") as f:
-            f.write("\n".join(edits.get(i, l) for i, l in enumerate(lines)))
-        obj2 = os.path.join(td, "out.o")
-        assemble(dst, obj2)
-        with open(dst) as f:
-            lines2 = f.read().split("\n")
-        check_blocks(lines, lines2)
-        where2 = source_insts(lines2)
-        for sym, insts in disassemble(obj2).items():
-            if sym not in loops:
-                continue
-            loop = hot_loop(insts, inner_headers(lines2, where2[sym]))
-            good, n = stats(insts, *loop)
-            if report:
-                print(f"  after: {sym[:60]:60s} {good}/{n}")
-            if good != n and not NO_NOP:
-                raise SystemExit(f"{sym}: {n - good} 8-byte VALU instructions not at {PHASE} mod 8")
+    return [edits.get(i, l) for i, l in enumerate(lines)], placed
+
+
+def misplaced(lines):
+    """{kernel: 8-byte VALU instructions of its placed loops not at PHASE mod 8}."""
+    with tempfile.TemporaryDirectory() as td:
+        path, obj = os.path.join(td, "out.s"), os.path.join(td, "out.o")
+        with open(path, "w") as f:
+            f.write("\n".join(lines))
+        assemble(path, obj)
+        funcs = disassemble(obj)
+    # the placed text may hold several instructions per line (s_nop + op)
+    lines = "\n".join(lines).split("\n")
+    where = source_insts(lines)
+    bad = {}
+    for sym, insts in funcs.items():
+        if sym not in where:
+            continue
+        for lp in kernel_loops(sym, insts, inner_headers(lines, where[sym])):
+            good, n = stats(insts, *lp)
+            if good != n:
+                bad[sym] = bad.get(sym, 0) + n - good
+    return bad
+
+
+def main():
+    global PHASE, NO_NOP, ALL_E64
+    src, dst = sys.argv[1], sys.argv[2]
+    report = "--report" in sys.argv
+    if "--phase" in sys.argv:
+        PHASE = int(sys.argv[sys.argv.index("--phase") + 1])
+    NO_NOP = "--no-nop" in sys.argv
+    ALL_E64 = "--keep-e32" not in sys.argv
+    with open(src) as f:
+        lines = f.read().split("\n")
+    out, placed = place(lines, report)
+    # an alignment directive between two loops of one kernel can absorb the
+    # bytes an earlier loop's edits add: place again until every loop holds
+    for _ in range(4):
+        bad = misplaced(out)
+        if not bad or NO_NOP:
+            break
+        out, _ = place("\n".join(out).split("\n"), report)
+    with open(dst, "w") as f:
+        f.write("\n".join(out))
+    with open(dst) as f:
+        lines2 = f.read().split("\n")
+    check_blocks(lines, lines2)
+    bad = misplaced(lines2)
+    if report:
+        for sym, n in placed.items():
+            print(f"  after: {sym[:60]:60s} {n} loop(s), {bad.get(sym, 0)} 8-byte VALU off {PHASE} mod 8")
+    if bad and not NO_NOP:
+        raise SystemExit(f"8-byte VALU instructions not at {PHASE} mod 8: {bad}")
 
 
 if __name__ == "__main__":

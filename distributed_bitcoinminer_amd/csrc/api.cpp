@@ -48,6 +48,11 @@ constexpr int kStreams = 4;
 // segments concurrently on all streams; larger ones use the dominant-stream
 // order with tail filling (enqueue_device_batch).
 constexpr uint64_t kConcurrentNonces = 1ull << 27;
+// Workgroups per CU of a fused (small-request) launch: a task takes ~1/3 the
+// wall time it takes at the 6 per CU that occupancy allows, so the launch
+// tail is ~3x shorter, at < 1 % of issue rate (profiles/r05/small_requests).
+constexpr int kFusedPerCu = 2;
+constexpr uint32_t kFusedDefaultFlags = 0;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -84,6 +89,7 @@ struct Device {
     hipStream_t stream[kStreams] = {};
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
+    uint32_t* aux[kStreams] = {};      // fused launches: s0 / trailer / K+W tables
     uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
     std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed after the call's waits
     uint64_t* cand[kStreams] = {};
@@ -134,6 +140,8 @@ struct hm_ctx {
     int table_digits = 0;    // HM_OPT_TABLE_DIGITS (test hook; 0 = default, -1 = off)
     uint64_t table_rows_cap = 0;  // HM_OPT_TABLE_ROWS_CAP (test hook; 0 = off)
     bool test_mid_sync = false;   // HM_OPT_TEST_MID_SYNC (test hook: a host wait mid-enqueue)
+    bool fused = true;            // HM_OPT_FUSED: small requests in one launch
+    uint32_t fused_flags = kFusedDefaultFlags;  // HM_OPT_FUSED_FLAGS (experiment hook)
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -176,6 +184,7 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
         dv.kwt_rows[s] = kMaxChainedTable;
+        HIPCHK(hipMalloc(&dv.aux[s], (size_t)kFusedAuxWords * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
         HIPCHK(hipMalloc(&dv.sums[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
@@ -200,6 +209,7 @@ void device_free(Device& dv) {
         if (dv.rec[s]) (void)hipFree(dv.rec[s]);
         if (dv.cand[s]) (void)hipFree(dv.cand[s]);
         if (dv.kwt[s]) (void)hipFree(dv.kwt[s]);
+        if (dv.aux[s]) (void)hipFree(dv.aux[s]);
         if (dv.counter[s]) (void)hipFree(dv.counter[s]);
         if (dv.sums[s]) (void)hipFree(dv.sums[s]);
         if (dv.join[s]) (void)hipEventDestroy(dv.join[s]);
@@ -231,6 +241,10 @@ std::string tiled_symbol(const SegPlan& s, bool csum) {
 const char* chained_symbol(bool csum) {
     return csum ? "_ZN2hm22hm_chained_csum_kernelENS_11ChainedArgsE"
                 : "_ZN2hm17hm_chained_kernelENS_11ChainedArgsE";
+}
+const char* fused_symbol(bool csum) {
+    return csum ? "_ZN2hm20hm_fused_csum_kernelENS_9FusedArgsE"
+                : "_ZN2hm15hm_fused_kernelENS_9FusedArgsE";
 }
 const char* generic_symbol(bool csum) {
     return csum ? "_ZN2hm22hm_generic_csum_kernelENS_11GenericArgsE"
@@ -623,6 +637,179 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
     return HM_OK;
 }
 
+// Fused launch (kernels.hpp, fused_kernels.hip): can all of a request's
+// segments run in one launch?  Up to kFusedNonces nonces and 20 segments;
+// tiled and generic segments always, chained ones with one table of f <= 4
+// digits (no epochs) whose rows fit the stream's aux buffer.
+bool fusible(const std::vector<SegPlan>& segs) {
+    if (segs.empty() || segs.size() > (size_t)kMaxFusedSegs) return false;
+    long double n = 0;
+    uint64_t rows = 0, tiles = 0;
+    for (const auto& g : segs) {
+        n += (long double)(g.hi - g.lo) + 1;
+        if (g.kind == HM_KIND_CHAINED) {
+            if (g.f > kMaxChainedF || g.fe != g.f) return false;
+            rows += pow10_u64(g.f);
+        }
+        if (g.kind != HM_KIND_GENERIC) tiles += g.tile_hi - g.tile_lo + 1;
+    }
+    return n <= (long double)kFusedNonces && rows <= kFusedKwRows && tiles <= kMaxTilesPerLaunch;
+}
+
+// Per-task cost rank of a segment's layout in the fused launch: the queue
+// hands out the costly tasks first, so the launch ends on the cheapest ones.
+int fused_rank(const SegPlan& g) {
+    if (g.kind == HM_KIND_CHAINED) return 0;   // 64 lanes x up to 100 blocks
+    if (g.kind == HM_KIND_GENERIC) return 1;   // 640 nonces, full tail compressions
+    return g.trailer ? 2 : 3;                  // 640 nonces, 2 or 1 compressions
+}
+
+// Enqueue every segment of one request as ONE fused launch on stream si:
+// hm_fused_plan_kernel (records, tables, counter; and, when `seed_best`, the
+// (MaxUint64, 0) seed of *best and zeroed coverage sums) -> hm_fused_kernel
+// -> hm_fold_kernel into *best.  Tasks are ordered costliest layout first,
+// larger segments first.
+int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPlan> segs, int si,
+                  uint64_t* best, bool seed_best) {
+    hipStream_t st = dv.stream[si];
+    std::stable_sort(segs.begin(), segs.end(), [](const SegPlan& a, const SegPlan& b) {
+        if (fused_rank(a) != fused_rank(b)) return fused_rank(a) < fused_rank(b);
+        return a.hi - a.lo > b.hi - b.lo;
+    });
+    FusedPlanArgs pa;
+    memset(&pa, 0, sizeof pa);
+    FusedArgs fa;
+    memset(&fa, 0, sizeof fa);
+    pa.rec = dv.rec[si];
+    pa.aux = dv.aux[si];
+    pa.counter = dv.counter[si];
+    pa.result = seed_best ? best : nullptr;
+    // a lone request (seed_best) also zeroes every stream's coverage sums,
+    // which hm_scan_checked adds up; in a batch they were zeroed up front
+    // and hold the other requests' sums
+    pa.acc = ctx->csum && seed_best ? dv.acc : nullptr;
+    pa.n_acc = 2 * kStreams;
+    pa.r = mp.r;
+    memcpy(pa.pw, mp.pw, sizeof pa.pw);
+    memcpy(pa.mid, mp.mid, sizeof pa.mid);
+    fa.rec = dv.rec[si];
+    fa.aux = dv.aux[si];
+    fa.counter = dv.counter[si];
+    fa.cand = dv.cand[si];
+    fa.sums = ctx->csum ? dv.sums[si] : nullptr;
+    fa.r = mp.r;
+    memcpy(fa.pw, mp.pw, sizeof fa.pw);
+    memcpy(fa.mid, mp.mid, sizeof fa.mid);
+    uint64_t tasks = 0, jobs = 0, nonces = 0;
+    uint32_t rec_next = 0, aux_next = 0, comp_max = 1;
+    double comp_w = 0;  // executed compressions x nonces (hm_stats)
+    for (size_t i = 0; i < segs.size(); ++i) {
+        const SegPlan& g = segs[i];
+        FusedSeg& S = fa.segs[i];
+        FusedPlanSeg& P = pa.segs[i];
+        const uint64_t cnt = g.hi - g.lo + 1;  // one digit count: far below 2^64
+        S.seg_lo = g.lo;
+        S.seg_hi = g.hi;
+        S.total_bits = g.total_bits;
+        S.d = g.d;
+        S.nb = g.nb;
+        P.total_bits = g.total_bits;
+        P.d = g.d;
+        P.nb = g.nb;
+        P.T = g.T;
+        P.V = g.V;
+        P.straddle = g.straddle;
+        P.loop_shift = g.loop_shift;
+        P.f = g.f;
+        uint64_t seg_tasks = 0, seg_jobs = 0;
+        double ce = (double)g.nb;
+        if (g.kind == HM_KIND_TILED || g.kind == HM_KIND_CHAINED) {
+            const bool ch = g.kind == HM_KIND_CHAINED;
+            const uint64_t nt = g.tile_hi - g.tile_lo + 1;
+            uint32_t unit0;
+            uint64_t nunits;
+            launch_units(g, g.tile_lo, nt, ch ? g.ntc : 1, ch ? pow10_u64(g.f) : 100, &unit0, &nunits);
+            S.tile0 = P.tile0 = g.tile_lo;
+            S.pow10V = P.pow10V = g.pow10V;
+            S.rec0 = P.rec0 = rec_next;
+            S.aux0 = P.aux0 = aux_next;
+            S.unit0 = unit0;
+            S.tpt = g.tpt;
+            S.vmax = (uint32_t)(pow10_u64(g.q) - 1);
+            S.q = g.q;
+            P.ntiles = (uint32_t)nt;
+            rec_next += (uint32_t)nt;
+            if (ch) {
+                S.variant = P.variant = kVarChained;
+                S.pow10f = pow10_u64(g.f);
+                S.ntc = g.ntc;
+                S.tch = g.tch;
+                S.tpu = (g.tch + kFusedChainedPiece - 1) / kFusedChainedPiece;
+                P.fb = 0;  // tail block 0 kept raw: its compression is per lane
+                seg_tasks = nunits * S.tpu;
+                seg_jobs = nt + pow10_u64(g.f);
+                aux_next += (uint32_t)pow10_u64(g.f) * 64;
+                ce = 1.0 + (double)seg_tasks / ((double)nunits * (double)g.tch);
+            } else {
+                S.variant = P.variant = (uint32_t)(g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0));
+                S.lane_shift = g.lane_shift;
+                S.loop_shift = g.loop_shift;
+                P.fb = g.fb;
+                seg_tasks = nunits * 10;
+                seg_jobs = nt + 100 + (g.trailer ? 1 : 0);
+                aux_next += 100 + (g.trailer ? 64 : 0);
+                ce = executed_compressions(g);
+            }
+        } else {
+            S.variant = P.variant = kVarGeneric;
+            seg_tasks = (cnt + 639) / 640;
+        }
+        tasks += seg_tasks;
+        jobs += seg_jobs;
+        S.task_end = (uint32_t)tasks;
+        P.job_end = (uint32_t)jobs;
+        nonces += cnt;
+        comp_max = std::max(comp_max, g.nb);
+        comp_w += ce * (double)cnt;
+    }
+    if (tasks >= (1ull << 31) || jobs >= (1ull << 31) || aux_next > kFusedAuxWords)
+        return HM_ERR_INTERNAL;  // excluded by fusible()
+    fa.ntasks = (uint32_t)tasks;
+    fa.nseg = pa.nseg = (uint32_t)segs.size();
+    pa.njobs = (uint32_t)jobs;
+    const Device::Fn* fn = nullptr;
+    int rc = scan_fn(dv, fused_symbol(ctx->csum), &fn);
+    if (rc) return rc;
+    // small launches: few waves per SIMD keep a task short, so the launch's
+    // tail is short (2 workgroups per CU, profiles/r05/small_requests)
+    const int grid = persistent_grid(ctx, dv, kFusedPerCu, tasks);
+    fa.flags = ctx->fused_flags;
+    // with static first tasks the queue starts past every wave slot
+    pa.counter0 = (fa.flags & kFusedStaticFirst) ? (uint32_t)grid * (kBlock / kWaveSize) : 0;
+    HIPCHK(launch_fused_plan(pa, st));
+    Launch L;
+    rc = next_event(dv, &L.start);
+    if (rc) return rc;
+    rc = next_event(dv, &L.stop);
+    if (rc) return rc;
+    L.nonces = nonces;
+    L.kind = HM_KIND_FUSED;
+    snprintf(L.kernel, sizeof L.kernel, ctx->csum ? "hm_fused_csum_kernel" : "hm_fused_kernel");
+    L.grid = grid;
+    L.compressions = comp_max;
+    L.comp_eff = comp_w / (double)nonces;
+    HIPCHK(hipEventRecord(L.start, st));
+    rc = launch_scan(*fn, fa, grid, st);
+    if (rc) return rc;
+    HIPCHK(hipEventRecord(L.stop, st));
+    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best, st));
+    if (ctx->csum)
+        HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize), dv.acc + 2 * si,
+                               st));
+    dv.launches.push_back(L);
+    return HM_OK;
+}
+
 struct DevReq {
     const MsgPlan* mp;
     uint64_t lo, hi;
@@ -638,6 +825,14 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     const int n = (int)reqs.size();
     hipStream_t s0 = dv.stream[0];
     if (first) HIPCHK(hipEventRecord(dv.t0, s0));
+    // one small request (config 1, short server chunks): the fused launch on
+    // stream 0 alone, its planner seeding the result slot -- nothing else
+    // runs between the call's first launch and the 16-B readback
+    if (n == 1 && !reqs[0].empty && ctx->fused && !ctx->test_mid_sync) {
+        std::vector<SegPlan> segs = plan_range(*reqs[0].mp, reqs[0].lo, reqs[0].hi,
+                                               ctx->force_generic, ctx->table_digits);
+        if (fusible(segs)) return enqueue_fused(ctx, dv, *reqs[0].mp, segs, 0, dv.result, true);
+    }
     HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
     HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
     if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
@@ -681,6 +876,13 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
             if (p.second > most) { most = p.second; dom = p.first; }
         }
         uint64_t* best = dv.best + (size_t)r * kStreams * 2;
+        if (ctx->fused && fusible(segs)) {
+            // a small request of a batch: one fused launch on the next stream
+            const int si = rr++ % nstreams;
+            int rc = enqueue_fused(ctx, dv, *reqs[r].mp, segs, si, best + 2 * si, false);
+            if (rc) return rc;
+            continue;
+        }
         if (nstreams > 1 && total <= (long double)kConcurrentNonces) {
             // a small request (config 1's [0, 10^7+1], short server chunks):
             // its launches are latency-bound, so every segment goes onto the
@@ -972,6 +1174,13 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
             return HM_OK;
         case HM_OPT_TEST_MID_SYNC:
             ctx->test_mid_sync = value != 0;
+            return HM_OK;
+        case HM_OPT_FUSED:
+            ctx->fused = value != 0;
+            return HM_OK;
+        case HM_OPT_FUSED_FLAGS:
+            if (value < 0 || value > 3) return HM_ERR_INVALID;
+            ctx->fused_flags = (uint32_t)value;
             return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;

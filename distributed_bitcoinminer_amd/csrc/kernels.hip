@@ -74,6 +74,81 @@ __global__ void __launch_bounds__(kBlock) hm_kw_table_kernel(uint32_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// Fused launch planner: one thread per job.  Per segment (FusedPlanSeg, in
+// job order): its tile records (as hm_tile_plan_kernel); then, tiled, the
+// 100 sigma0 values of the loop-digit bits (tiled_loop_sigma0 in plan.cpp)
+// and, with a trailer, the trailer block's 64 K+W words (one job); chained,
+// its 10^f K+W rows (as hm_kw_table_kernel, without epochs).  Thread 0 also
+// resets the queue counter, seeds the result slot and zeroes the checked
+// scans' accumulators, so nothing else runs between this and the scan.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) hm_fused_plan_kernel(const FusedPlanArgs A) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g == 0) {
+        *A.counter = A.counter0;
+        if (A.result) { A.result[0] = ~0ull; A.result[1] = 0; }  // miner.go:48-49
+        for (uint32_t i = 0; A.acc && i < A.n_acc; ++i) A.acc[i] = 0;
+    }
+    if (g >= A.njobs) return;
+    uint32_t si = 0;
+    while (g >= A.segs[si].job_end) ++si;
+    const FusedPlanSeg& S = A.segs[si];
+    uint32_t j = g - (si ? A.segs[si - 1].job_end : 0);
+    if (j < S.ntiles) {
+        uint32_t w[32];
+        build_tail(w, A.pw, A.r, S.d, S.V, (S.tile0 + j) * S.pow10V, S.nb, S.total_bits);
+        uint32_t st[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) st[k] = A.mid[k];
+        uint32_t* out = A.rec + (size_t)(S.rec0 + j) * kRecWords;
+        if (S.fb == 1) {
+            h_compress(st, w);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) out[8 + k] = w[16 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) out[8 + k] = w[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) out[k] = st[k];
+        return;
+    }
+    j -= S.ntiles;
+    uint32_t* aux = A.aux + S.aux0;
+    if (S.variant == kVarChained) {
+        // K+W row j of the final block holding the f digits of j
+        uint32_t b[32];
+        const uint32_t zero[16] = {0};
+        build_tail(b, zero, 0, S.f, 0, j, 1, S.total_bits);
+        uint32_t w[64];
+#pragma unroll
+        for (int k = 0; k < 64; ++k) w[k] = k < 16 ? b[k] : 0u;
+        h_schedule(w);
+        uint32_t* o = aux + (size_t)j * 64;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) o[k] = kK[k] + w[k];
+        return;
+    }
+    if (j < 100) {  // tiled: sigma0 of the loop digits' bits of W[W1], t1 * 10 + t0
+        const uint32_t t1 = j / 10, t0 = j - t1 * 10;
+        const uint32_t L = S.straddle ? (0x30u + t0) << 24
+                                      : (((0x30u + t1) << 8) | (0x30u + t0)) << S.loop_shift;
+        aux[j] = h_rotr(L, 7) ^ h_rotr(L, 18) ^ (L >> 3);
+        return;
+    }
+    // tiled with a trailer: K+W of the constant padding block (trailer_kw)
+    uint32_t w[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) w[k] = 0;
+    if (S.T == 64) w[0] = 0x80000000u;  // 0x80 opens the trailer block
+    w[14] = (uint32_t)(S.total_bits >> 32);
+    w[15] = (uint32_t)S.total_bits;
+    h_schedule(w);
+#pragma unroll
+    for (int k = 0; k < 64; ++k) aux[100 + k] = kK[k] + w[k];
+}
+
+// ---------------------------------------------------------------------------
 // Second reduce pass and init
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restrict__ cand,
@@ -148,6 +223,12 @@ hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
                        uint32_t stride) {
     hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, stride, best);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_plan(const FusedPlanArgs& a, hipStream_t s) {
+    const uint32_t grid = a.njobs ? (a.njobs + kBlock - 1) / kBlock : 1;
+    hipLaunchKernelGGL(hm_fused_plan_kernel, dim3(grid), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

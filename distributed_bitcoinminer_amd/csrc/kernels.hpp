@@ -107,6 +107,82 @@ struct GenericArgs {
     uint32_t mid[8];
 };
 
+// ---------------------------------------------------------------------------
+// Fused small requests (DESIGN.md §3 "Fused launch"): every digit segment of
+// one request of <= kFusedNonces nonces in ONE persistent launch.  A task
+// names its segment by its id (task_end is cumulative); each segment runs
+// its own layout's task body (scan_tasks.hpp), selected per task by a
+// wave-uniform switch on `variant`.  One planner launch first writes every
+// segment's tile records and tables (s0_loop, trailer K+W, chained K+W rows)
+// and resets the queue counter and the result slot.
+// ---------------------------------------------------------------------------
+constexpr int kMaxFusedSegs = 20;          // digit counts of a u64 nonce
+constexpr uint64_t kFusedNonces = 1ull << 27;  // requests up to this size are fused
+constexpr uint32_t kFusedKwRows = 12288;   // chained K+W rows per stream (f <= 4: <= 11110)
+constexpr uint32_t kFusedAuxWords = kFusedKwRows * 64 + kMaxFusedSegs * 164;
+constexpr uint32_t kFusedChainedPiece = 100;  // loop values per chained task
+// variant ids: tiled W1 * 4 + 2 * straddle + trailer (4..63), then:
+constexpr uint32_t kVarChained = 64;
+constexpr uint32_t kVarGeneric = 65;
+
+struct FusedSeg {
+    uint64_t tile0;       // absolute index of the segment's first tile (tiled, chained)
+    uint64_t pow10V;      // nonces per tile
+    uint64_t pow10f;      // chained: nonces per lane value (10^f)
+    uint64_t seg_lo, seg_hi;
+    uint64_t total_bits;  // generic: message bit length
+    uint32_t task_end;    // one past the segment's last task id (cumulative)
+    uint32_t variant;
+    uint32_t rec0;        // the segment's first record in FusedArgs::rec
+    uint32_t aux0;        // word offset of its tables in FusedArgs::aux
+    uint32_t unit0;       // first unit kept (edge trimming, launch_units)
+    uint32_t tpt;         // lane chunks per tile
+    uint32_t vmax, q;
+    uint32_t lane_shift, loop_shift;  // tiled
+    uint32_t ntc, tch, tpu;  // chained: loop chunks per lane chunk, values per chunk, tasks per unit
+    uint32_t d, nb;       // generic: digits, tail blocks
+};
+
+// FusedArgs::flags (HM_OPT_FUSED_FLAGS): how waves get their tasks
+constexpr uint32_t kFusedStaticFirst = 1;  // first task = the wave's slot; the counter starts past them
+constexpr uint32_t kFusedPrefetch = 2;     // dequeue the next task id while running the current one
+
+struct FusedArgs {
+    const uint32_t* rec;
+    const uint32_t* aux;
+    unsigned int* counter;
+    uint64_t* cand;
+    uint64_t* sums;       // checked scans only
+    uint32_t ntasks, nseg;
+    uint32_t flags;       // kFused*
+    uint32_t r;           // prefix-remainder bytes (generic)
+    uint32_t pw[16];      // prefix remainder words (generic)
+    uint32_t mid[8];      // midstate (generic)
+    FusedSeg segs[kMaxFusedSegs];
+};
+
+struct FusedPlanSeg {
+    uint64_t tile0, pow10V, total_bits;
+    uint32_t job_end;     // one past the segment's last planner job (cumulative)
+    uint32_t ntiles, rec0, aux0;
+    uint32_t V, d, fb, nb, T;
+    uint32_t variant, straddle, loop_shift, f;
+};
+
+struct FusedPlanArgs {
+    uint32_t* rec;
+    uint32_t* aux;
+    unsigned int* counter;  // reset to counter0
+    uint32_t counter0;
+    uint64_t* result;       // if set: seeded (MaxUint64, 0)
+    uint64_t* acc;          // if set (checked scans): [n_acc] zeroed
+    uint32_t n_acc;
+    uint32_t njobs, nseg, r;
+    uint32_t pw[16];
+    uint32_t mid[8];
+    FusedPlanSeg segs[kMaxFusedSegs];
+};
+
 // Launchers of the auxiliary kernels (kernels.hip; return hipError_t of the
 // launch).  The scan kernels (scan_kernels.hip: hm_tiled_kernel<W1,
 // STRADDLE, TRAILER>, hm_chained_kernel, hm_generic_kernel and their
@@ -124,5 +200,7 @@ hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
                        uint32_t stride = 1);
 hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);
+// The fused launch's planner: tile records, tables, counter/result/acc reset.
+hipError_t launch_fused_plan(const FusedPlanArgs& a, hipStream_t s);
 
 }  // namespace hm

@@ -136,6 +136,8 @@ typedef struct hm_stats {
 #define HM_KIND_GENERIC 1  /* one nonce per lane, generic tail builder          */
 #define HM_KIND_TILED 2    /* tile-planned final block (lane + loop digits)      */
 #define HM_KIND_CHAINED 3  /* two-block tail: per-lane block 0, table-driven final block */
+#define HM_KIND_FUSED 4    /* every segment of a small request in one launch, each
+                              with its own layout's task body (ABI 1.7)          */
 
 /* Options for hm_set_option. */
 #define HM_OPT_FORCE_GENERIC 1 /* 1: route every segment to the generic kernel  */
@@ -167,6 +169,16 @@ typedef struct hm_stats {
                                   each device's first queued work while still
                                   enqueuing, which hm_stats.mid_call_syncs must
                                   count (ABI 1.7)                               */
+#define HM_OPT_FUSED 10         /* 1 (default): a request (per device shard) of at
+                                  most 2^27 nonces whose segments all fit the
+                                  fused launch runs as ONE planner + ONE scan
+                                  launch (HM_KIND_FUSED); 0: one launch per
+                                  digit segment (ABI 1.7)                       */
+#define HM_OPT_FUSED_FLAGS 11   /* experiment hook (0..3): how the fused launch's
+                                  waves get tasks -- bit 0: first task = the
+                                  wave's slot (no opening burst of queue
+                                  atomics); bit 1: dequeue the next task while
+                                  the current one runs (ABI 1.7)                */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */

@@ -1,0 +1,130 @@
+"""The fused small-request launch (ABI 1.7, HM_KIND_FUSED) on the GPU.
+
+A request of <= 2^27 nonces whose segments all fit runs as ONE planner
+launch and ONE scan launch (fused_kernels.hip), each segment with its own
+layout's task body.  Here: configs[0]'s Request (the client's [0, 10^7] plus
+the server's +1, cmu440/bitcoin/server/server.go:169) is one launch; every
+message length 0..130 (every tail layout: tiled with and without a trailer,
+chained f <= 4, generic) is checked with the coverage checksum against the C
+oracle, fused and per-segment; batches mix fused and per-segment requests;
+and the edges (empty, single nonce, 2^64-1, forced generic) hold.  The
+reference loop: cmu440/bitcoin/miner/miner.go:46-59 over bitcoin.Hash
+(hash.go:13-17)."""
+import random
+
+import pytest
+
+from distributed_bitcoinminer_amd import _lib
+
+pytestmark = pytest.mark.gpu
+MAX = (1 << 64) - 1
+
+
+@pytest.fixture()
+def fused_off(ctx):
+    ctx.set_option(_lib.HM_OPT_FUSED, 0)
+    yield ctx
+    ctx.set_option(_lib.HM_OPT_FUSED, 1)
+
+
+def test_config1_is_one_launch(ctx):
+    assert ctx.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+    st = ctx.stats()
+    assert st["launches"] == 1 and st["dom_kind"] == _lib.HM_KIND_FUSED, st
+    assert st["dom_kernel"] == "hm_fused_kernel" and st["nonces"] == 10**7 + 2, st
+    assert st["dom_compressions_eff"] == 1.0, st
+
+
+def test_config1_per_segment_path_still_answers(fused_off):
+    assert fused_off.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+    st = fused_off.stats()
+    assert st["launches"] == 8 and st["dom_kind"] == _lib.HM_KIND_TILED, st
+
+
+def test_every_layout_checked_vs_oracle(ctx, oracle_mod):
+    """Every message length 0..130 over a range crossing a digit-count change:
+    the fused launch's (min, key sum, count) equals the oracle's, and so does
+    the per-segment path's."""
+    rng = random.Random(505)
+    kinds = set()
+    for L in range(131):
+        m = bytes(rng.randrange(32, 127) for _ in range(L))
+        d = rng.randrange(2, 20)
+        lo = max(0, 10**d - rng.randrange(1, 25_000))
+        hi = min(MAX, 10**d + rng.randrange(0, 25_000))
+        exp = oracle_mod.c_scan_sum(m, lo, hi)
+        got = ctx.scan_checked(m, lo, hi)
+        assert got == exp, (L, lo, hi)
+        assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
+        kinds |= {s["kind"] for s in _lib.debug_plan(m, lo, hi)}
+        ctx.set_option(_lib.HM_OPT_FUSED, 0)
+        try:
+            assert ctx.scan_checked(m, lo, hi) == exp, ("per-segment", L, lo, hi)
+        finally:
+            ctx.set_option(_lib.HM_OPT_FUSED, 1)
+    assert kinds >= {_lib.HM_KIND_TILED, _lib.HM_KIND_CHAINED, _lib.HM_KIND_GENERIC}
+
+
+def test_layouts_with_trailer_and_chained_segments(ctx, oracle_mod):
+    """Messages whose segments use the trailer block (45-55 B at d = 10) and
+    the chained layout (f = 1..4), several segments per request."""
+    rng = random.Random(606)
+    for L in (44, 45, 50, 54, 55, 56, 57, 60, 63, 64, 100, 119, 120, 127):
+        m = bytes(rng.randrange(33, 127) for _ in range(L))
+        for lo, hi in ((0, 2_000_000), (10**9 - 700_000, 10**9 + 700_000),
+                       (10**11 - 300_000, 10**11 + 900_000)):
+            assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, lo, hi)
+            st = ctx.stats()
+            assert st["launches"] == 1 and st["dom_kind"] == _lib.HM_KIND_FUSED, st
+
+
+def test_random_requests_vs_oracle(ctx, oracle_mod):
+    """200 random (message, range) draws of up to 2e5 nonces, anywhere in u64."""
+    rng = random.Random(707)
+    for _ in range(200):
+        m = bytes(rng.randrange(256) for _ in range(rng.randrange(131)))
+        if rng.random() < 0.6:
+            lo = max(0, 10**rng.randrange(1, 20) - rng.randrange(1, 100_000))
+        else:
+            lo = rng.randrange(MAX)
+        hi = min(MAX, lo + rng.randrange(200_000))
+        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (m.hex(), lo, hi)
+
+
+def test_edges(ctx, oracle_mod):
+    assert ctx.scan(b"bradfitz", 5, 4) == (MAX, 0)
+    for n in (0, 9, 10, 10**19, MAX):
+        assert ctx.scan(b"x", n, n) == (oracle_mod.c_hash(b"x", n), n)
+    lo = MAX - 150_000
+    assert ctx.scan_checked(b"bradfitz", lo, MAX) == oracle_mod.c_scan_sum(b"bradfitz", lo, MAX)
+    assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
+    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+    try:
+        for m, lo, hi in ((b"bradfitz", 0, 200_000), (b"y" * 60, 10**9 - 5000, 10**9 + 5000)):
+            assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi)
+            st = ctx.stats()
+            assert st["launches"] == 1 and st["dom_kind"] == _lib.HM_KIND_FUSED, st
+    finally:
+        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+
+
+def test_batch_mixes_fused_and_per_segment_requests(ctx, oracle_mod):
+    """hm_scan_many: small requests go to fused launches on the stream
+    round-robin, a large one to the per-segment path; all answers exact."""
+    reqs = [(b"bradfitz", 0, 10**6), (b"thom yorke", 10**9 - 10**5, 10**9 + 10**5),
+            (b"q" * 61, 10**12, 10**12 + 3 * 10**5), (b"bradfitz", 10**9, 10**9 + 3 * 10**8),
+            (b"", 0, 99), (b"z" * 120, 10**7 - 10**5, 10**7 + 10**5)]
+    exp = [oracle_mod.c_scan(m, lo, hi) for m, lo, hi in reqs]
+    assert ctx.scan_many(reqs) == exp
+    st = ctx.stats()
+    assert st["launches"] >= 5 + 1, st
+
+
+def test_multi_device_context_fuses_each_shard(oracle_mod):
+    """Context([0, 0]): each device's shard of a small request is one fused
+    launch; the merged answer equals the oracle's."""
+    with _lib.Context([0, 0]) as c:
+        m, lo, hi = b"bradfitz", 0, 3_000_000
+        assert c.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi)
+        st = c.stats()
+        assert st["launches"] == 2 and st["dom_kind"] == _lib.HM_KIND_FUSED, st

@@ -262,12 +262,21 @@ def test_stats_accounting(ctx):
     # of its loop: 1 + 1/tch compressions per nonce (tch = 1000 for f = 3)
     rng = random.Random(440)
     long120 = bytes(rng.choice(range(0x21, 0x7F)) for _ in range(120))
-    ctx.scan(long120, 10**9, 10**9 + 10**8)
+    ctx.set_option(_lib.HM_OPT_FUSED, 0)  # 10^8 nonces: a fused launch by default
+    try:
+        ctx.scan(long120, 10**9, 10**9 + 10**8)
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED, 1)
     st = ctx.stats()
     assert st["dom_kind"] == _lib.HM_KIND_CHAINED and st["dom_compressions"] == 2
     # counted exactly (ABI 1.5): one block-0 compression per task and lane;
     # whole units cost 1/1000 per loop value, guided-split ones 10/1000
     assert 1.001 <= st["dom_compressions_eff"] <= 1.01
+    # the fused launch: chained tasks of 100 loop values (block 0 per 100)
+    ctx.scan(long120, 10**9, 10**9 + 10**8)
+    st = ctx.stats()
+    assert st["dom_kind"] == _lib.HM_KIND_FUSED and st["dom_compressions"] == 2
+    assert 1.009 <= st["dom_compressions_eff"] <= 1.011
     # a scan_many batch over several chunks times every launch against one
     # origin: the union of launch intervals is positive and below the wall time
     ctx.scan_many([(b"bradfitz", 10**9 + 10**7 * i, 10**9 + 10**7 * (i + 1) - 1)
