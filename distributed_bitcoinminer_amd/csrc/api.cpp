@@ -48,11 +48,13 @@ constexpr int kStreams = 4;
 // segments concurrently on all streams; larger ones use the dominant-stream
 // order with tail filling (enqueue_device_batch).
 constexpr uint64_t kConcurrentNonces = 1ull << 27;
-// Workgroups per CU of a fused (small-request) launch: a task takes ~1/3 the
-// wall time it takes at the 6 per CU that occupancy allows, so the launch
-// tail is ~3x shorter, at < 1 % of issue rate (profiles/r05/small_requests).
-constexpr int kFusedPerCu = 2;
-constexpr uint32_t kFusedDefaultFlags = 0;
+// Workgroups per CU of a fused (small-request) launch: fewer waves per SIMD
+// than occupancy allows (6), so a task's wall time, and with it the launch's
+// tail, is about halved at < 1 % of issue rate; first tasks handed out by
+// wave slot (no opening burst of queue atomics).  Interleaved A/B over
+// flags x grids: profiles/r05/fused/fused_ab.jsonl.
+constexpr int kFusedPerCu = 3;
+constexpr uint32_t kFusedDefaultFlags = kFusedStaticFirst;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception

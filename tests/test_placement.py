@@ -129,3 +129,26 @@ def test_shipped_scan_kernels_are_placed():
         assert loop is not None, sym
         good, n = al.stats(insts, *loop)
         assert good == n and n > 300, (sym, good, n)
+
+
+FUSED = os.path.join(ROOT, "build", "hipminer", "fused_kernels.aligned.s")
+
+
+@pytest.mark.skipif(not os.path.exists(FUSED), reason="library not built")
+def test_shipped_fused_kernel_loops_are_placed():
+    """The fused small-request kernel holds one hot loop per segment layout
+    (32 tiled, chained, generic); the pass places every one of them."""
+    with open(FUSED) as f:
+        lines = f.read().split("\n")
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        obj = os.path.join(td, "a.o")
+        al.assemble(FUSED, obj)
+        funcs = al.disassemble(obj)
+    where = al.source_insts(lines)
+    sym = next(s for s in where if "hm_fused_kernel" in s)
+    loops = al.kernel_loops(sym, funcs[sym], al.inner_headers(lines, where[sym]))
+    assert len(loops) >= 34, len(loops)
+    for lp in loops:
+        good, n = al.stats(funcs[sym], *lp)
+        assert good == n and n > 300, (lp, good, n)

@@ -2,6 +2,10 @@
 import sys, time, json
 sys.path.insert(0, '.')
 from distributed_bitcoinminer_amd import _lib
+if "--lib" in sys.argv:  # an experiment build (tools/build_variant.sh)
+    i = sys.argv.index("--lib")
+    _lib.LIB_PATH = sys.argv[i + 1]
+    del sys.argv[i:i + 2]
 c = _lib.Context([0])
 msg = sys.argv[1].encode() if len(sys.argv) > 1 else b"bradfitz"
 lo = int(sys.argv[2]) if len(sys.argv) > 2 else 0
