@@ -358,17 +358,30 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
-// Host wait for stream st: the ONLY host wait on GPU work in a scan call
-// (the result readback; device_free at hm_close is outside any call).
-// Counted in hm_stats.mid_call_syncs when the call is still enqueuing work
-// (on this or a later device): such a wait would hold back every launch after
-// it.  No enqueue path calls it (HM_OPT_TEST_MID_SYNC makes one, so tests can
-// see the counter work); nothing on the enqueue path blocks on GPU work
-// otherwise: launches, event records, async memsets, hipMalloc of a grown
-// table (no wait on queued work).
+// The host-blocking HIP calls of a scan call -- a stream wait, a free (hipFree
+// waits for the whole device) and a synchronous readback -- go through these
+// three helpers and nowhere else (device_free at hm_close is outside any
+// call; tests/test_abi.py checks the sources for stray ones).  Each counts in
+// hm_stats.mid_call_syncs when the call is still enqueuing work (on this or a
+// later device): such a wait would hold back every launch after it.  No
+// enqueue path calls them (HM_OPT_TEST_MID_SYNC makes one, so tests can see
+// the counter work).  The enqueue path's only other host call that is not an
+// async launch, event record or memset is hipMalloc of a grown K+W table
+// (hm_stats.table_grows), which does not wait for queued work
+// (tests/test_gpu_enqueue.py bounds enqueue_ms against the call's wall).
 int host_wait(hm_ctx* ctx, hipStream_t st) {
     if (ctx->enqueuing) ++ctx->mid_syncs;
     HIPCHK(hipStreamSynchronize(st));
+    return HM_OK;
+}
+int host_free(hm_ctx* ctx, void* p) {
+    if (ctx->enqueuing) ++ctx->mid_syncs;
+    HIPCHK(hipFree(p));
+    return HM_OK;
+}
+int host_read(hm_ctx* ctx, void* dst, const void* src, size_t n) {
+    if (ctx->enqueuing) ++ctx->mid_syncs;
+    HIPCHK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return HM_OK;
 }
 
@@ -405,7 +418,10 @@ int free_retired(hm_ctx* ctx) {
     for (auto& dv : ctx->devs) {
         if (dv.retired.empty()) continue;
         HIPCHK(hipSetDevice(dv.ordinal));
-        for (uint32_t* t : dv.retired) HIPCHK(hipFree(t));
+        for (uint32_t* t : dv.retired) {
+            int rc = host_free(ctx, t);
+            if (rc) return rc;
+        }
         dv.retired.clear();
     }
     return HM_OK;
@@ -1323,7 +1339,8 @@ int hm_scan_checked(hm_ctx* ctx, const uint8_t* msg, size_t len, uint64_t lo, ui
     for (auto& dv : ctx->devs) {
         uint64_t a[kStreams * 2];
         HIPCHK(hipSetDevice(dv.ordinal));
-        HIPCHK(hipMemcpy(a, dv.acc, sizeof a, hipMemcpyDeviceToHost));
+        rc = host_read(ctx, a, dv.acc, sizeof a);
+        if (rc) return rc;
         for (int i = 0; i < kStreams; ++i) { s += a[2 * i]; c += a[2 * i + 1]; }
     }
     *out = res;

@@ -168,3 +168,30 @@ def test_scan_stats_writes_only_the_frozen_144_bytes(ctx):
     buf2 = (ctypes.c_uint8 * 256)(*([0xA5] * 256))
     assert lib.hm_scan_stats_sized(ctx._h, ctypes.cast(buf2, ctypes.POINTER(_lib.hm_stats)), 160) == 0
     assert all(b == 0xA5 for b in buf2[160:]) and bytes(buf2[:144]) == bytes(buf[:144])
+
+
+def test_host_blocking_calls_only_in_counting_helpers():
+    """hm_stats.mid_call_syncs counts host waits issued while a call is still
+    enqueuing.  That holds by construction only if every host-blocking HIP
+    call of the library (stream/device/event waits, hipFree, synchronous
+    hipMemcpy) sits in the counting helpers host_wait / host_free / host_read,
+    or in device_free (hm_close, outside any call).  Scan every C++ source of
+    the library for stray ones."""
+    import re
+    csrc = os.path.join(os.path.dirname(_lib.__file__), "csrc")
+    blocking = re.compile(r"\b(hipStreamSynchronize|hipDeviceSynchronize|hipEventSynchronize|"
+                          r"hipFree|hipMemcpy)\s*\(")
+    allowed = {"host_wait", "host_free", "host_read", "device_free"}
+    func = re.compile(r"^[A-Za-z_][\w:<>*& ]*?\b(\w+)\s*\([^;]*\)\s*(const\s*)?\{\s*$")
+    stray = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".cpp", ".hpp")):
+            continue
+        current = None
+        for no, line in enumerate(open(os.path.join(csrc, name)), 1):
+            m = func.match(line)
+            if m:
+                current = m.group(1)
+            if blocking.search(line) and current not in allowed:
+                stray.append(f"{name}:{no} in {current}: {line.strip()}")
+    assert not stray, stray
