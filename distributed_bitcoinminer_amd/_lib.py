@@ -31,6 +31,7 @@ HM_OPT_TABLE_ROWS_CAP = 8
 HM_OPT_TEST_MID_SYNC = 9
 HM_OPT_FUSED = 10
 HM_OPT_FUSED_FLAGS = 11
+HM_OPT_FUSED_PARTS = 12
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 

@@ -55,6 +55,7 @@ constexpr uint64_t kConcurrentNonces = 1ull << 27;
 // flags x grids: profiles/r05/fused/fused_ab.jsonl.
 constexpr int kFusedPerCu = 3;
 constexpr uint32_t kFusedDefaultFlags = kFusedStaticFirst;
+constexpr uint32_t kFusedDefaultParts = 1;  // tiled fused tasks: one tens digit (10 steps)
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -144,6 +145,7 @@ struct hm_ctx {
     bool test_mid_sync = false;   // HM_OPT_TEST_MID_SYNC (test hook: a host wait mid-enqueue)
     bool fused = true;            // HM_OPT_FUSED: small requests in one launch
     uint32_t fused_flags = kFusedDefaultFlags;  // HM_OPT_FUSED_FLAGS (experiment hook)
+    uint32_t fused_parts = kFusedDefaultParts;  // HM_OPT_FUSED_PARTS (experiment hook)
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -772,8 +774,9 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
                 S.variant = P.variant = (uint32_t)(g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0));
                 S.lane_shift = g.lane_shift;
                 S.loop_shift = g.loop_shift;
+                S.tpu = ctx->fused_parts;
                 P.fb = g.fb;
-                seg_tasks = nunits * 10;
+                seg_tasks = nunits * 10 * ctx->fused_parts;
                 seg_jobs = nt + 100 + (g.trailer ? 1 : 0);
                 aux_next += 100 + (g.trailer ? 64 : 0);
                 ce = executed_compressions(g);
@@ -799,7 +802,7 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     int rc = scan_fn(dv, fused_symbol(ctx->csum), &fn);
     if (rc) return rc;
     // small launches: few waves per SIMD keep a task short, so the launch's
-    // tail is short (2 workgroups per CU, profiles/r05/small_requests)
+    // tail is short (kFusedPerCu = 3 workgroups per CU, profiles/r05/fused/)
     const int grid = persistent_grid(ctx, dv, kFusedPerCu, tasks);
     fa.flags = ctx->fused_flags;
     // with static first tasks the queue starts past every wave slot
@@ -1199,6 +1202,10 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
         case HM_OPT_FUSED_FLAGS:
             if (value < 0 || value > 3) return HM_ERR_INVALID;
             ctx->fused_flags = (uint32_t)value;
+            return HM_OK;
+        case HM_OPT_FUSED_PARTS:
+            if (value != 1 && value != 2 && value != 5 && value != 10) return HM_ERR_INVALID;
+            ctx->fused_parts = (uint32_t)value;
             return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;

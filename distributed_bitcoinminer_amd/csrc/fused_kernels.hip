@@ -11,7 +11,8 @@
 // task runs that segment's layout -- the same task bodies as the
 // per-segment kernels (scan_tasks.hpp), chosen by a wave-uniform switch:
 //   tiled  (any W1 / straddle / trailer): one unit's lane chunk x one tens
-//          digit (64 lanes x 10 nonces), as the per-segment kernel's tail;
+//          digit (64 lanes x 10 nonces), as the per-segment kernel's tail,
+//          or a part of it (FusedSeg::tpu parts, HM_OPT_FUSED_PARTS);
 //   chained (f <= 4 final-block digits, one K+W table): 64 lanes x up to
 //          100 table-driven blocks, block 0 per lane per task;
 //   generic: 64 lanes x 10 nonces, the byte-level tail builder.
@@ -38,15 +39,21 @@ typedef const __attribute__((address_space(4))) FusedArgs FusedArgsK;
 template <int W1, bool STRADDLE, bool TRAILER, bool CSUM>
 DEV void fused_tiled(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& best,
                      WaveSums& sums) {
-    const uint32_t unit = S.unit0 + k / 10u;
-    const uint32_t t1 = k - (k / 10u) * 10u;
+    // task k: unit, tens digit t1 and part of the units loop (S.tpu parts
+    // of 10 / S.tpu steps each)
+    const uint32_t per_unit = 10u * S.tpu;
+    const uint32_t unit = S.unit0 + k / per_unit;
+    const uint32_t rem = k - (k / per_unit) * per_unit;
+    const uint32_t t1 = rem / S.tpu;
+    const uint32_t part = rem - t1 * S.tpu;
+    const uint32_t steps = 10u / S.tpu;
     const uint32_t tile = unit / S.tpt;
     const uint32_t chunk = unit - tile * S.tpt;
     const_u32* tab = (const_u32*)(A->aux + S.aux0);
     tiled_task<W1, STRADDLE, TRAILER, CSUM>(A->rec + (size_t)(S.rec0 + tile) * kRecWords, chunk, t1,
                                             t1 + 1, (S.tile0 + tile) * S.pow10V, S.seg_lo, S.seg_hi,
                                             S.vmax, S.q, S.lane_shift, S.loop_shift, tab, tab + 100,
-                                            best, sums);
+                                            best, sums, part * steps, part * steps + steps);
 }
 
 template <bool CSUM>

@@ -139,7 +139,8 @@ struct FusedSeg {
     uint32_t tpt;         // lane chunks per tile
     uint32_t vmax, q;
     uint32_t lane_shift, loop_shift;  // tiled
-    uint32_t ntc, tch, tpu;  // chained: loop chunks per lane chunk, values per chunk, tasks per unit
+    uint32_t ntc, tch;    // chained: loop chunks per lane chunk, values per chunk
+    uint32_t tpu;         // chained: tasks per unit; tiled: parts per tens digit (1, 2, 5, 10)
     uint32_t d, nb;       // generic: digits, tail blocks
 };
 

@@ -71,12 +71,16 @@ DEV uint64_t lane_digits(uint32_t v, uint32_t q) {
 // SHA-256 compression per nonce from the tile state (+ a constant trailer
 // block, table kw, when the padding spills).  s0_loop[t1*10 + t0] = sigma0
 // of the loop-digit bits of W[W1] (wave-uniform, read by scalar loads).
+// t0 runs over [t0_begin, t0_end) (the fused launch's split tasks; the
+// per-segment kernels take the constant defaults, so their loop is the full
+// one).
 // ---------------------------------------------------------------------------
 template <int W1, bool STRADDLE, bool TRAILER, bool CSUM, typename S0, typename KW>
 DEV void tiled_task(const uint32_t* __restrict__ R, uint32_t chunk, uint32_t t1_begin,
                     uint32_t t1_end, uint64_t tile_base, uint64_t seg_lo, uint64_t seg_hi,
                     uint32_t vmax, uint32_t q, uint32_t lane_shift, uint32_t loop_shift,
-                    S0 s0_loop, KW trailer_kw, WaveBest& best, WaveSums& sums) {
+                    S0 s0_loop, KW trailer_kw, WaveBest& best, WaveSums& sums,
+                    uint32_t t0_begin = 0, uint32_t t0_end = 10) {
     static_assert(W1 >= 1 && W1 <= 15, "varying words are W[W1-1], W[W1]");
     // Lane digits may reach back into W[W1-2] (the planner does so when the
     // last two words leave room for fewer than 5 lane digits: 10^3 or 10^4
@@ -138,7 +142,7 @@ DEV void tiled_task(const uint32_t* __restrict__ R, uint32_t chunk, uint32_t t1_
         const uint32_t T2 = bsig0<false>(s1.a) + maj(s1.a, s1.b, s1.c);
         uint32_t dP = s1.d + P, PT = P + T2;
         asm volatile("" : "+v"(dP), "+v"(PT));
-        for (uint32_t t0 = 0; t0 < 10; ++t0) {
+        for (uint32_t t0 = t0_begin; t0 < t0_end; ++t0) {
             uint32_t m[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) m[k] = mw[k];

@@ -179,6 +179,9 @@ typedef struct hm_stats {
                                   wave's slot (no opening burst of queue
                                   atomics); bit 1: dequeue the next task while
                                   the current one runs (ABI 1.7)                */
+#define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
+                                  tiled task of the fused launch covers 10 /
+                                  parts steps of its units loop (ABI 1.7)       */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */

@@ -128,3 +128,29 @@ def test_multi_device_context_fuses_each_shard(oracle_mod):
         assert c.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi)
         st = c.stats()
         assert st["launches"] == 2 and st["dom_kind"] == _lib.HM_KIND_FUSED, st
+
+
+@pytest.mark.parametrize("parts", [2, 5, 10])
+def test_split_tiled_tasks_checked(ctx, oracle_mod, parts):
+    """HM_OPT_FUSED_PARTS: tiled tasks of the fused launch cut into `parts`
+    pieces of the units loop; (min, key sum, count) over tiled layouts with
+    and without trailer / straddle, several segments per request, still
+    equal the oracle's."""
+    rng = random.Random(808 + parts)
+    ctx.set_option(_lib.HM_OPT_FUSED_PARTS, parts)
+    try:
+        assert ctx.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+        for L in (0, 8, 13, 30, 45, 50, 55, 61, 70, 110):
+            m = bytes(rng.randrange(33, 127) for _ in range(L))
+            lo = max(0, 10**rng.randrange(3, 19) - rng.randrange(1, 400_000))
+            hi = lo + rng.randrange(1, 800_000)
+            assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, lo, hi)
+            assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED_PARTS, 1)
+
+
+def test_fused_parts_option_validated(ctx):
+    for bad in (0, 3, 4, 11, -1):
+        with pytest.raises(_lib.HipMinerError):
+            ctx.set_option(_lib.HM_OPT_FUSED_PARTS, bad)

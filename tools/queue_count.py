@@ -1,0 +1,70 @@
+"""Count this process's GPU user-mode queues (dev tool, GPU box) at each stage
+of what one rank of the N-GPU bench line does on its GPU, from KFD's
+per-process sysfs (/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/{gpuid,type}):
+torch's CUDA context, a torch stream, an RCCL (world-1) all-gather, a hipminer
+context with its 4 streams, the scan, and after hm_close.  DESIGN §6 uses the
+counts to price the processes and hardware queues per GPU of the N = 8 line.
+One JSON line per stage."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PROC = f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"
+
+
+def queues():
+    try:
+        qs = sorted(os.listdir(PROC), key=lambda s: int(s) if s.isdigit() else 0)
+    except OSError as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    out = []
+    for q in qs:
+        rec = {"qid": q}
+        for f in ("gpuid", "type", "size"):
+            try:
+                with open(os.path.join(PROC, q, f)) as fh:
+                    rec[f] = fh.read().strip()
+            except OSError:
+                pass
+        out.append(rec)
+    return {"count": len(out), "queues": out}
+
+
+def stage(name):
+    print(json.dumps({"stage": name, **queues()}), flush=True)
+
+
+def main():
+    stage("start")
+    import torch
+    torch.zeros(1, device="cuda:0")
+    torch.cuda.synchronize()
+    stage("torch context (null stream, one kernel)")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        torch.ones(1, device="cuda:0").add_(1)
+    torch.cuda.synchronize()
+    stage("torch side stream")
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    out = [torch.zeros(2, dtype=torch.int64, device="cuda:0")]
+    dist.all_gather(out, torch.ones(2, dtype=torch.int64, device="cuda:0"))
+    torch.cuda.synchronize()
+    stage("RCCL world-1 all-gather")
+    from distributed_bitcoinminer_amd import _lib
+    c = _lib.Context([0])
+    stage("hm_open (4 streams)")
+    c.scan(b"bradfitz", 0, 10**8)
+    stage("hm_scan [0, 10^8]")
+    c.close()
+    stage("hm_close")
+    dist.destroy_process_group()
+    stage("destroy_process_group")
+
+
+if __name__ == "__main__":
+    main()
