@@ -126,18 +126,29 @@ DEV void fused_body(FusedArgsK* A) {
     WaveBest best;
     WaveSums sums;  // CSUM only
     const uint32_t flags = A->flags;
+    const uint32_t nwaves = gridDim.x * (kBlock / kWaveSize);
+    __shared__ LdsQueue queue;  // kFusedLds
+    if (flags & kFusedLds) lds_queue_init(&queue);
     // task ids: with kFusedStaticFirst the first is the wave's slot (the
     // planner started the counter past every slot), so the launch opens
     // without a burst of queue atomics; with kFusedPrefetch the next id is
-    // dequeued before the current task runs, hiding the atomic's latency
-    uint32_t next = 0;
-    if (flags & kFusedStaticFirst) next = wslot;
-    else if (__lane_id() == 0) next = atomicAdd(A->counter, 1u);
+    // dequeued before the current task runs, hiding the atomic's latency;
+    // kFusedLds dequeues through the workgroup's LDS dispenser (one queue
+    // atomic per 4 tasks); kFusedStatic strides the wave slots over the task
+    // ids (wslot, wslot + nwaves, ...) with no queue at all
+    auto dequeue = [&]() -> uint32_t {
+        if (flags & kFusedLds) return lds_dequeue(&queue, A->counter);
+        uint32_t t = 0;
+        if (__lane_id() == 0) t = atomicAdd(A->counter, 1u);
+        return t;
+    };
+    uint32_t next = (flags & (kFusedStaticFirst | kFusedStatic)) ? wslot : dequeue();
     for (;;) {
         const uint32_t task = uni(next);
         if (task >= A->ntasks) break;
         next = 0;
-        if ((flags & kFusedPrefetch) && __lane_id() == 0) next = atomicAdd(A->counter, 1u);
+        if (flags & kFusedStatic) next = task + nwaves;
+        else if (flags & kFusedPrefetch) next = dequeue();
         uint32_t i = 0;
         while (i + 1 < A->nseg && task >= A->segs[i].task_end) ++i;
         const FusedSeg S_ = A->segs[i];  // scalar loads of one descriptor
@@ -162,7 +173,7 @@ DEV void fused_body(FusedArgsK* A) {
             case kVarChained: fused_chained<CSUM>(A, S_, k, best, sums); break;
             default: fused_generic<CSUM>(A, S_, k, best, sums); break;
         }
-        if (!(flags & kFusedPrefetch) && __lane_id() == 0) next = atomicAdd(A->counter, 1u);
+        if (!(flags & (kFusedPrefetch | kFusedStatic))) next = dequeue();
     }
     wave_store<CSUM>(A->cand, A->sums, wslot, best, sums);
 }

@@ -147,6 +147,8 @@ struct FusedSeg {
 // FusedArgs::flags (HM_OPT_FUSED_FLAGS): how waves get their tasks
 constexpr uint32_t kFusedStaticFirst = 1;  // first task = the wave's slot; the counter starts past them
 constexpr uint32_t kFusedPrefetch = 2;     // dequeue the next task id while running the current one
+constexpr uint32_t kFusedStatic = 4;       // no queue: wave w runs tasks w, w + nwaves, w + 2 nwaves, ...
+constexpr uint32_t kFusedLds = 8;          // dequeue through the workgroup's LDS dispenser (scan_tasks.hpp)
 
 struct FusedArgs {
     const uint32_t* rec;

@@ -45,50 +45,6 @@ namespace hm {
 #define HM_TILED_BOUNDS __launch_bounds__(kBlock)
 #endif
 
-// Workgroup-level task dispenser (round 5).  A wave draws a ticket from an
-// LDS counter; the first ticket of each batch of kLdsBatch fetches the
-// batch's task ids from the launch's queue with ONE device-scope atomic and
-// publishes the base in a 4-entry LDS ring; the batch's other tickets wait
-// for it there (at most one atomic's round trip, the waves of a workgroup
-// rarely finish a task together).  The per-wave task granularity and the
-// guided tail are unchanged; the queue sees a quarter of the atomics, which
-// execute memory-side (PMC WRITE_SIZE per cfg2 launch 18.1 -> 4.6 MB; cfg2
-// +0.1 %, cfg3 +1.0 %, d = 12 +0.04 % in an interleaved A/B,
-// profiles/r05/experiments/lds_dispenser/).  The ring cannot be lapped: a
-// batch's slot is rewritten only 16 tickets later, and each of the 4 waves
-// holds one ticket at a time.
-constexpr uint32_t kLdsBatch = 4;
-struct LdsQueue {
-    uint32_t ticket;
-    uint32_t base[4];
-    uint32_t ready[4];  // batch + 1 once base[batch & 3] is set
-};
-DEV void lds_queue_init(LdsQueue* q) {
-    if (threadIdx.x == 0) {
-        q->ticket = 0;
-        for (int i = 0; i < 4; ++i) q->ready[i] = 0;
-    }
-    __syncthreads();
-}
-DEV uint32_t lds_dequeue(LdsQueue* q, unsigned int* counter) {
-    uint32_t task = 0;
-    if (__lane_id() == 0) {
-        const uint32_t t = atomicAdd(&q->ticket, 1u);
-        const uint32_t batch = t / kLdsBatch, slot = batch & 3u;
-        if (t - batch * kLdsBatch == 0) {
-            q->base[slot] = atomicAdd(counter, kLdsBatch);
-            __hip_atomic_store(&q->ready[slot], batch + 1, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            while (__hip_atomic_load(&q->ready[slot], __ATOMIC_ACQUIRE,
-                                     __HIP_MEMORY_SCOPE_WORKGROUP) != batch + 1)
-                __builtin_amdgcn_s_sleep(2);
-        }
-        task = q->base[slot] + (t - batch * kLdsBatch);
-    }
-    return uni(task);
-}
-
 // CSUM: checked variant (coverage sum and count of the hashed keys).
 template <int W1, bool STRADDLE, bool TRAILER, bool CSUM>
 DEV void tiled_body(const TiledArgs& A) {

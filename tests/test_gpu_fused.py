@@ -154,3 +154,23 @@ def test_fused_parts_option_validated(ctx):
     for bad in (0, 3, 4, 11, -1):
         with pytest.raises(_lib.HipMinerError):
             ctx.set_option(_lib.HM_OPT_FUSED_PARTS, bad)
+
+
+@pytest.mark.parametrize("flags", [0, 2, 3, 4, 8, 9])
+def test_task_dispensing_flags_checked(ctx, oracle_mod, flags):
+    """HM_OPT_FUSED_FLAGS: every way the fused launch's waves get their tasks
+    (queue, static first task, prefetch, static stride, LDS dispenser) hashes
+    every nonce once: (min, key sum, count) equal the oracle's, over layouts
+    with trailer, straddle, chained and generic segments."""
+    rng = random.Random(909 + flags)
+    ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, flags)
+    try:
+        assert ctx.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+        for L in (0, 8, 45, 55, 60, 61, 100, 120):
+            m = bytes(rng.randrange(33, 127) for _ in range(L))
+            lo = max(0, 10**rng.randrange(3, 19) - rng.randrange(1, 400_000))
+            hi = lo + rng.randrange(1, 1_500_000)
+            assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, lo, hi)
+            assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, 1)

@@ -35,7 +35,7 @@ HM_BENCH_STREAMS=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/seri
   -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-secondary > $O/bench_serial.json 2> $O/serial.log &&
 timeout -k 10 200 python -u tools/request_sizes.py > $O/request_sizes.jsonl 2> $O/request_sizes.err &&
 timeout -k 10 120 python -u tools/e2e_cfg1.py > $O/e2e_cfg1.json 2> $O/e2e_cfg1.err &&
-timeout -k 10 300 python -u tools/fused_ab.py 15 1 3,4,6 1,2,5 > $O/fused_parts_ab.jsonl 2> $O/fused_parts_ab.err &&
+timeout -k 10 300 python -u tools/fused_ab.py 15 ${FUSED_FLAGS:-1} ${FUSED_PER_CU:-3,4,6} ${FUSED_PARTS:-1,2,5} > $O/fused_parts_ab.jsonl 2> $O/fused_parts_ab.err &&
 timeout -k 10 240 python -u tools/coresident.py --sweep 0,1,3,5,7,11 --streams 1 > $O/coresident_s1.jsonl 2> $O/coresident_s1.err &&
 timeout -k 10 240 python -u tools/coresident.py --sweep 0,3,5,7,11 --streams 4 > $O/coresident_s4.jsonl 2> $O/coresident_s4.err
 rc=$?

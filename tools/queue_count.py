@@ -11,12 +11,33 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PROC = f"/sys/class/kfd/kfd/proc/{os.getpid()}/queues"
+KFD = "/sys/class/kfd/kfd/proc"
+# KFD names its per-process directories by HOST pid, which a container's pid
+# is not: this process's directory is the one that appears when it first
+# opens the GPU (the box runs nothing else of ours meanwhile)
+BEFORE = set()
+MINE = []
+
+
+def _listing():
+    try:
+        return set(os.listdir(KFD))
+    except OSError:
+        return None
 
 
 def queues():
+    if not MINE:
+        now = _listing()
+        if now is None:
+            return {"error": f"{KFD} not readable"}
+        new = sorted(now - BEFORE)
+        if len(new) != 1:
+            return {"error": f"{len(new)} new KFD process directories", "new": new[:8]}
+        MINE.append(new[0])
+    d = os.path.join(KFD, MINE[0], "queues")
     try:
-        qs = sorted(os.listdir(PROC), key=lambda s: int(s) if s.isdigit() else 0)
+        qs = sorted(os.listdir(d), key=lambda s: int(s) if s.isdigit() else 0)
     except OSError as e:
         return {"error": f"{type(e).__name__}: {e}"}
     out = []
@@ -24,12 +45,12 @@ def queues():
         rec = {"qid": q}
         for f in ("gpuid", "type", "size"):
             try:
-                with open(os.path.join(PROC, q, f)) as fh:
+                with open(os.path.join(d, q, f)) as fh:
                     rec[f] = fh.read().strip()
             except OSError:
                 pass
         out.append(rec)
-    return {"count": len(out), "queues": out}
+    return {"kfd_pid": MINE[0], "count": len(out), "queues": out}
 
 
 def stage(name):
@@ -37,7 +58,8 @@ def stage(name):
 
 
 def main():
-    stage("start")
+    BEFORE.update(_listing() or ())
+    print(json.dumps({"stage": "start", "kfd_processes": len(BEFORE)}), flush=True)
     import torch
     torch.zeros(1, device="cuda:0")
     torch.cuda.synchronize()
