@@ -60,8 +60,12 @@ def _per_rank(ranks, n, ordinals=None):
 
 
 def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
+    """Also the multi-rank single-process pass: rank 1 parks in the host-side
+    wait group while rank 0 runs both children (HM_BENCH_SP_DEVICES=0: one
+    context on GPU 0, host merge and a 1-rank RCCL merge)."""
     line = _torchrun(2, ["--steps", "1", "--warmup", "0", "--secondary", "cfg4",
-                         "--no-cpu-baseline"], {"HM_BENCH_BACKEND": "gloo"}, timeout=420)
+                         "--no-cpu-baseline"],
+                     {"HM_BENCH_BACKEND": "gloo", "HM_BENCH_SP_DEVICES": "0"}, timeout=600)
     assert line["n_gpus"] == 2 and line["config"]["merge"] == "gloo"
     assert line["result_vs_oracle"]["match"] is True, line["result_vs_oracle"]
     assert len(line["ranks"]["local_ms"]) == 2
@@ -82,6 +86,13 @@ def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
     from distributed_bitcoinminer_amd import _lib
     lo, hi = _lib.partition(b"bradfitz", 0, (1 << 40) - 1, 2)[0]
     assert c4["nonces_rank0"] == hi - lo + 1
+    sp = line["single_process"]
+    assert sp["processes_per_gpu"] == {"0": 3}, sp  # both ranks and the child
+    for m, merge in (("host", "none"), ("rccl", "RCCL all-gather")):
+        e = sp[m]
+        assert "error" not in e, e
+        assert e["devices"] == [0] and e["merge"] == merge, e
+        assert e["result_vs_oracle"]["match"] is True and e["mid_call_syncs"] == 0, e
 
 
 def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
