@@ -479,7 +479,8 @@ def roofline(st, msg, lo, hi):
     achieved_rounds = nonces_pl * rops / (avg_ms * 1e-3) / 1e12
     # algorithmic HBM bytes of one dominant launch: its 128-B tile records
     # (10^V nonces each) + one 16-B candidate per wave of the grid; the
-    # work queue adds one device-scope atomicAdd per dequeued task
+    # work queue adds one device-scope atomicAdd per 4 dequeued tasks (the
+    # workgroup's LDS dispenser, scan_tasks.hpp kLdsBatch)
     tiles_pl = -(-int(nonces_pl) // 10 ** dom_seg["V"])
     algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
     tasks_pl = int(nonces_pl) // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
@@ -495,9 +496,10 @@ def roofline(st, msg, lo, hi):
             "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": algo_bytes,
-            "queue_atomics_per_launch": tasks_pl,
+            "queue_units_per_launch": tasks_pl,
+            "queue_atomics_per_launch": -(-tasks_pl // 4) if tasks_pl is not None else None,
             "traffic_note": "PMC traffic is the work queue's device-scope atomics "
-                            "(one per dequeued task, executed memory-side), not "
+                            "(one per 4 dequeued tasks, executed memory-side), not "
                             "re-reads (DESIGN.md §9)",
             "f_eff_ghz": f_eff,
             "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
