@@ -16,6 +16,7 @@
 // recompressed only when a carry reaches it.  The compression uses the x86
 // SHA extensions when the CPU has them (HM_CPU_NO_SHA=1 forces the portable
 // C compression, for tests), else the planner's h_compress.
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -160,6 +161,18 @@ void scan_chunk(const MsgPlan& mp, uint64_t a, uint64_t b, CompressFn compress, 
     *out = best;
 }
 
+// Default thread count: the CPUs this process may run on.  A GPU box's
+// per-GPU share is an affinity set inside a machine whose
+// hardware_concurrency() counts every CPU, many times more.
+unsigned default_threads() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) {
+        const int c = CPU_COUNT(&set);
+        if (c > 0) return (unsigned)c;
+    }
+    return std::max(1u, std::thread::hardware_concurrency());
+}
+
 }  // namespace
 }  // namespace hm
 
@@ -177,7 +190,7 @@ extern "C" int hm_scan_cpu(const uint8_t* msg, size_t len, uint64_t lo, uint64_t
         const CompressFn compress = pick_compress();
         typedef unsigned __int128 u128;
         const u128 count = (u128)(hi - lo) + 1;
-        unsigned n = threads > 0 ? (unsigned)threads : std::max(1u, std::thread::hardware_concurrency());
+        unsigned n = threads > 0 ? (unsigned)threads : default_threads();
         n = std::min(n, 1024u);
         if (count < (u128)n * 4096) n = (unsigned)std::max<u128>(1, count / 4096);
         std::vector<Best> part(n);

@@ -255,8 +255,9 @@ int hm_scan_stats_sized(const hm_ctx *ctx, hm_stats *out, size_t size);
 /* The same scan as hm_scan -- lexicographic min of (Hash(msg, n), n) over
  * the INCLUSIVE [lo, hi], seeded (UINT64_MAX, 0), bit-identical -- on the
  * host's cores, without a GPU (ABI 1.7; SURVEY §8(b)'s liveness path).
- * `threads` <= 0 uses every hardware thread; the range is split into that
- * many contiguous chunks (ranges below 4096 nonces per thread use fewer).
+ * `threads` <= 0 uses one thread per CPU this process may run on (its
+ * affinity mask, at most 1024); the range is split into that many
+ * contiguous chunks (ranges below 4096 nonces per thread use fewer).
  * x86 SHA extensions when the CPU has them (HM_CPU_NO_SHA=1 forces portable
  * C).  Orders of magnitude slower than hm_scan: for callers whose GPU is
  * missing or failed (hm_miner, the Go gpuminer), so a Result is still
