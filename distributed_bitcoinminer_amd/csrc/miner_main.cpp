@@ -16,7 +16,10 @@
 // (server.go:326-376).  Only a bad HIPMINER_DEVICES list ends the process.
 //
 // Env: HIPMINER_DEVICES=0,1 (default: all visible), HM_CPU_THREADS (host
-// scan threads, default every hardware thread), HM_LSP_* (lsp_client.hpp).
+// scan threads, default the CPUs of the process's affinity mask), HM_LSP_*
+// (lsp_client.hpp).  Test hook: HM_MINER_TEST_FAIL_AFTER=N treats the GPU
+// scan of the (N+1)-th Request as failed (HM_ERR_HIP, no hm_scan call), so
+// tests can drive the mid-run fallback (tests/test_gpu_miner_lsp.py).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -72,6 +75,8 @@ int main(int argc, char** argv) {
     }
     const char* th = getenv("HM_CPU_THREADS");
     const int cpu_threads = th ? atoi(th) : 0;
+    const char* fa = getenv("HM_MINER_TEST_FAIL_AFTER");
+    long gpu_scans_left = fa && *fa ? atol(fa) : -1;  // < 0: no injected failure
     if (rc != HM_OK) {
         gpu = nullptr;
         fprintf(stderr, "hm_miner: NO GPU (%s): every Request is scanned on the host "
@@ -100,7 +105,10 @@ int main(int argc, char** argv) {
                 hm_result out;
                 rc = HM_ERR_NO_DEVICE;
                 if (gpu) {
-                    rc = hm_scan(gpu, msg, req.data.size(), req.lower, end - 1, &out);
+                    rc = gpu_scans_left == 0
+                             ? HM_ERR_HIP
+                             : hm_scan(gpu, msg, req.data.size(), req.lower, end - 1, &out);
+                    if (gpu_scans_left > 0) --gpu_scans_left;
                     if (rc != HM_OK) {
                         fprintf(stderr, "hm_miner: GPU scan FAILED (%s): this and every later "
                                         "Request are scanned on the host (hm_scan_cpu)\n",

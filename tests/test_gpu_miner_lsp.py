@@ -210,3 +210,34 @@ def test_server_sim_reassigns_a_killed_miner(oracle_mod):
                 p.wait(timeout=60)
             except subprocess.TimeoutExpired:
                 p.kill()
+
+
+def test_miner_falls_back_to_host_after_a_failed_gpu_scan(oracle_mod):
+    """SURVEY §8(b) liveness, mid-run: the GPU answers the first Request, the
+    second GPU scan fails (HM_MINER_TEST_FAIL_AFTER=1 injects HM_ERR_HIP), and
+    that Request and every later one are still answered, on the host
+    (hm_scan_cpu), with the oracle's Results; the miner says so on stderr."""
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=50)
+    env = dict(ENV, HM_MINER_TEST_FAIL_AFTER="1", HM_CPU_THREADS="8")
+    p = subprocess.Popen([MINER, srv.hostport], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        cid = srv.accept(timeout=120)
+        assert srv.read(cid, timeout=60) == bitcoin.marshal(bitcoin.NewJoin())
+        assert _ask(srv, cid, "bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)  # GPU
+        m = "thom yorke".encode()
+        assert _ask(srv, cid, m, 19970000, 19971000) == oracle_mod.c_scan(m, 19970000, 19971000)
+        assert _ask(srv, cid, b"x" * 120, MAX - 5000, MAX - 1) == \
+            oracle_mod.c_scan(b"x" * 120, MAX - 5000, MAX - 1)
+        assert _ask(srv, cid, "bradfitz", 0, MAX) == (MAX, 0)  # Upper+1 wraps: no scan
+    finally:
+        srv.close()
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    err = p.stderr.read()
+    assert p.returncode == 0, err
+    assert "GPU scan FAILED" in err and "hm_scan_cpu" in err, err
+    assert "NO GPU" not in err, err
