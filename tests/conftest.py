@@ -36,3 +36,18 @@ def ctx():
     c = _lib.Context([0])
     yield c
     c.close()
+
+
+@pytest.fixture(params=["fused", "per_segment"])
+def ctx_paths(request, ctx):
+    """The session context once per small-request path.  Since round 5 a
+    request of <= 2^27 nonces runs as ONE fused launch (HM_OPT_FUSED=1, the
+    default); HM_OPT_FUSED=0 sends the same request through the per-segment
+    kernels, which requests above 2^27 nonces always take.  Sweeps over small
+    ranges use this fixture so both paths keep their layout coverage."""
+    from distributed_bitcoinminer_amd import _lib
+    ctx.set_option(_lib.HM_OPT_FUSED, 1 if request.param == "fused" else 0)
+    try:
+        yield ctx
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED, 1)

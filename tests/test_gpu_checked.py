@@ -42,7 +42,7 @@ def _generic(ctx, m, lo, hi):
         ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
 
 
-def test_checked_golden(ctx, golden):
+def test_checked_golden(ctx_paths, golden):
     n = 0
     for case in golden["scan_kats"]:
         if "sum" not in case:
@@ -50,7 +50,7 @@ def test_checked_golden(ctx, golden):
         m = bytes.fromhex(case["msg_hex"])
         lo, hi = int(case["lo"]), int(case["hi"])
         exp = ((int(case["hash"]), int(case["nonce"])), int(case["sum"]), int(case["count"]))
-        assert ctx.scan_checked(m, lo, hi) == exp, (case["name"], lo, hi)
+        assert ctx_paths.scan_checked(m, lo, hi) == exp, (case["name"], lo, hi)
         n += 1
     assert n >= 390
 
@@ -62,7 +62,7 @@ def test_checked_min_equals_scan(ctx):
         assert best == ctx.scan(m, lo, hi) and cnt == hi - lo + 1
 
 
-def test_checked_layout_sweep_vs_oracle(ctx, oracle_mod):
+def test_checked_layout_sweep_vs_oracle(ctx_paths, oracle_mod):
     """Every message length 0..130 x every digit count, both ends of each digit
     segment (partial tiles, surplus lanes, digit-count changes)."""
     rng = random.Random(5)
@@ -72,10 +72,10 @@ def test_checked_layout_sweep_vs_oracle(ctx, oracle_mod):
             dlo = 0 if d == 1 else 10**(d - 1)
             dhi = min(10**d - 1, MAX)
             for lo, hi in ((dlo, min(dhi, dlo + 500)), (max(dlo, dhi - 400), min(MAX, dhi + 200))):
-                assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, d, lo, hi)
+                assert ctx_paths.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (L, d, lo, hi)
 
 
-def test_checked_whole_tiles_vs_generic(ctx):
+def test_checked_whole_tiles_vs_generic(ctx_paths):
     """Whole tiles of every fast layout (tiled / chained, W1, straddle, trailer,
     V) against the generic kernel's checked scan, including ranges large
     enough to use both whole and split (guided) tasks."""
@@ -94,23 +94,31 @@ def test_checked_whole_tiles_vs_generic(ctx):
             seen.add(key)
             span = min(3 * 10**seg["V"] + 4321, 6 * 10**7, (dhi - dlo) // 2)
             lo = rng.randrange(dlo, dhi - span)
-            fast = ctx.scan_checked(m, lo, lo + span)
-            assert fast == _generic(ctx, m, lo, lo + span), (L, d, key)
+            fast = ctx_paths.scan_checked(m, lo, lo + span)
+            assert fast == _generic(ctx_paths, m, lo, lo + span), (L, d, key)
             assert fast[2] == span + 1
     assert len(seen) >= 40, len(seen)
 
 
 def test_checked_guided_split_boundaries(ctx):
     """bradfitz d=10: units of 6400 nonces; around one unit per wave of the
-    grid the launch switches from whole units to tenths.  Ranges below, at and
-    above that size, cut at arbitrary points, add up exactly."""
+    grid the per-segment launch switches from whole units to tenths.  Ranges
+    below, at and above that size, cut at arbitrary points, add up exactly.
+    These ranges are small enough for the fused launch, so the per-segment
+    kernels are forced (HM_OPT_FUSED=0); the fused answer must agree."""
     base = 3_000_000_000 + 12_345
-    whole = ctx.scan_checked(b"bradfitz", base, base + 80_000_000)
     cuts = [base, base + 1, base + 6399, base + 20_000_000, base + 33_000_001,
             base + 64_000_000, base + 80_000_001]
-    parts = [ctx.scan_checked(b"bradfitz", a, b - 1) for a, b in zip(cuts, cuts[1:])]
+    ctx.set_option(_lib.HM_OPT_FUSED, 0)
+    try:
+        whole = ctx.scan_checked(b"bradfitz", base, base + 80_000_000)
+        assert ctx.stats()["dom_kind"] == _lib.HM_KIND_TILED
+        parts = [ctx.scan_checked(b"bradfitz", a, b - 1) for a, b in zip(cuts, cuts[1:])]
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED, 1)
     assert _add(parts) == whole
     assert whole == _generic(ctx, b"bradfitz", base, base + 80_000_000)
+    assert whole == ctx.scan_checked(b"bradfitz", base, base + 80_000_000)  # fused
 
 
 def _long120():

@@ -15,25 +15,25 @@ pytestmark = pytest.mark.gpu
 MAX = (1 << 64) - 1
 
 
-def test_golden_scans(ctx, golden):
+def test_golden_scans(ctx_paths, golden):
     for case in golden["scan_kats"]:
         m = bytes.fromhex(case["msg_hex"])
         lo, hi = int(case["lo"]), int(case["hi"])
-        got = ctx.scan(m, lo, hi)
+        got = ctx_paths.scan(m, lo, hi)
         assert got == (int(case["hash"]), int(case["nonce"])), (case["name"], lo, hi)
 
 
-def test_golden_scans_generic_kernel(ctx, golden):
-    ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+def test_golden_scans_generic_kernel(ctx_paths, golden):
+    ctx_paths.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
     try:
         for case in golden["scan_kats"][:60]:
             m = bytes.fromhex(case["msg_hex"])
             lo, hi = int(case["lo"]), int(case["hi"])
             if hi - lo > 2_000_000:
                 continue
-            assert ctx.scan(m, lo, hi) == (int(case["hash"]), int(case["nonce"])), case["name"]
+            assert ctx_paths.scan(m, lo, hi) == (int(case["hash"]), int(case["nonce"])), case["name"]
     finally:
-        ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+        ctx_paths.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
 
 
 def test_config1_answer(ctx):
@@ -55,7 +55,7 @@ def test_empty_range(ctx):
     assert ctx.scan(b"", MAX, 0) == (MAX, 0)
 
 
-def test_random_vs_oracle(ctx, oracle_mod):
+def test_random_vs_oracle(ctx_paths, oracle_mod):
     """Random messages (0..130 B, every tail layout) x ranges across digit boundaries."""
     rng = random.Random(2026)
     for it in range(120):
@@ -65,20 +65,20 @@ def test_random_vs_oracle(ctx, oracle_mod):
         c = 10 ** k
         lo = max(0, c - rng.randrange(0, 40000))
         hi = min(MAX, c + rng.randrange(0, 40000))
-        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
+        assert ctx_paths.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
 
 
-def test_tiles_vs_oracle_medium(ctx, oracle_mod):
+def test_tiles_vs_oracle_medium(ctx_paths, oracle_mod):
     """Ranges spanning whole tiles (10^5..10^8 nonces per tile) for assorted layouts."""
     rng = random.Random(7)
     for L in (0, 3, 8, 20, 44, 45, 50, 54, 55, 56, 60, 63, 64, 70, 100, 119, 120, 127):
         m = bytes(rng.randrange(32, 127) for _ in range(L))
         lo = rng.randrange(10**9, 10**12)
         hi = lo + 1_500_000
-        assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
+        assert ctx_paths.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, lo, hi)
 
 
-def test_chained_layouts_vs_oracle(ctx, oracle_mod):
+def test_chained_layouts_vs_oracle(ctx_paths, oracle_mod):
     """Two-block tails whose final block holds 1..4 digits (chained kernel)."""
     rng = random.Random(99)
     seen = set()
@@ -96,7 +96,7 @@ def test_chained_layouts_vs_oracle(ctx, oracle_mod):
             seen.add((T - 64, seg["V"] - (T - 64)))
             base = rng.randrange(10**(d - 1), dhi - 300_000)
             lo, hi = base, base + rng.randrange(1, 250_000)
-            assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
+            assert ctx_paths.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
     assert {(1, 5), (2, 5), (3, 5), (4, 5)} <= seen
 
 
@@ -298,7 +298,7 @@ def test_server_model_end_to_end_gpu(ctx, oracle_mod):
         assert got == oracle_mod.c_scan(msg, lo, chunks[-1][0])
 
 
-def test_layout_sweep_segment_edges(ctx, oracle_mod):
+def test_layout_sweep_segment_edges(ctx_paths, oracle_mod):
     """Every message length 0..130 x every digit count: small ranges at both
     ends of each digit segment (partial tiles, masking, digit-count changes)."""
     import random as _r
@@ -309,10 +309,10 @@ def test_layout_sweep_segment_edges(ctx, oracle_mod):
             dlo = 0 if d == 1 else 10**(d - 1)
             dhi = min(10**d - 1, MAX)
             for lo, hi in ((dlo, min(dhi, dlo + 700)), (max(dlo, dhi - 700), min(MAX, dhi + 300))):
-                assert ctx.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
+                assert ctx_paths.scan(m, lo, hi) == oracle_mod.c_scan(m, lo, hi), (L, d, lo, hi)
 
 
-def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
+def test_layout_sweep_full_tiles_tiled_vs_generic(ctx_paths):
     """Whole tiles (10^5..10^8 nonces) of every layout the planner picks for
     lengths 0..130: fast kernels vs the independent generic kernel."""
     import random as _r
@@ -331,12 +331,12 @@ def test_layout_sweep_full_tiles_tiled_vs_generic(ctx):
             seen.add(key)
             span = min(2 * 10**seg["V"] + 12345, 3 * 10**8, (dhi - dlo) // 2)
             lo = rng.randrange(dlo, dhi - span)
-            fast = ctx.scan(m, lo, lo + span)
-            ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
+            fast = ctx_paths.scan(m, lo, lo + span)
+            ctx_paths.set_option(_lib.HM_OPT_FORCE_GENERIC, 1)
             try:
-                slow = ctx.scan(m, lo, lo + span)
+                slow = ctx_paths.scan(m, lo, lo + span)
             finally:
-                ctx.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
+                ctx_paths.set_option(_lib.HM_OPT_FORCE_GENERIC, 0)
             assert fast == slow, (L, d, key)
             assert _lib.host_hash(m, fast[1]) == fast[0]
     assert len(seen) >= 40, len(seen)
