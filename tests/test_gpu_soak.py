@@ -11,7 +11,9 @@ digits over 1.3-3.2*10^7 nonces (the chained layout with a K+W table, round 3)
 under a random table cap HM_OPT_TABLE_DIGITS (1..5: 10^4..1 epochs).
 A second soak (half the budget) sends random hm_scan_many batches to fresh
 multi-"device" contexts under random stream counts and table-growth caps.
-HM_SOAK_SEED picks the sequence; a failure names its case.
+HM_SOAK_SEED picks the sequence; a failure names its case.  HM_SOAK_FUSED=0
+sends the small requests through the per-segment kernels instead of the fused
+launch (HM_OPT_FUSED=0), which every request above 2^27 nonces takes.
 Progress goes to stdout every ~10 s (run with -s).
 """
 import os
@@ -59,25 +61,31 @@ def test_random_soak_checked(ctx, oracle_mod):
     t0 = last = time.time()
     n = nonces = 0
     from distributed_bitcoinminer_amd import _lib
-    while time.time() - t0 < budget:
-        table = 0
-        if rng.randrange(5) == 0:
-            m, lo, hi, table = _epoch_case(rng)
-        else:
-            m, lo, hi = _case(rng)
-        ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, table)
-        try:
-            got = ctx.scan_checked(m, lo, hi)
-        finally:
-            ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
-        exp = oracle_mod.c_scan_sum(m, lo, hi)
-        assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi, table)
-        n += 1
-        nonces += hi - lo + 1
-        if time.time() - last > 10:
-            last = time.time()
-            print(f"soak: {n} cases, {nonces} nonces, {last - t0:.0f} s", flush=True)
-    print(f"soak done: seed {seed}, {n} cases, {nonces} nonces, all equal to the oracle", flush=True)
+    fused = os.environ.get("HM_SOAK_FUSED", "1") != "0"
+    ctx.set_option(_lib.HM_OPT_FUSED, 1 if fused else 0)
+    try:
+        while time.time() - t0 < budget:
+            table = 0
+            if rng.randrange(5) == 0:
+                m, lo, hi, table = _epoch_case(rng)
+            else:
+                m, lo, hi = _case(rng)
+            ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, table)
+            try:
+                got = ctx.scan_checked(m, lo, hi)
+            finally:
+                ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
+            exp = oracle_mod.c_scan_sum(m, lo, hi)
+            assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi, table)
+            n += 1
+            nonces += hi - lo + 1
+            if time.time() - last > 10:
+                last = time.time()
+                print(f"soak: {n} cases, {nonces} nonces, {last - t0:.0f} s", flush=True)
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED, 1)
+    print(f"soak done: seed {seed}, fused {int(fused)}, {n} cases, {nonces} nonces, "
+          "all equal to the oracle", flush=True)
     assert n > 0
 
 
@@ -112,6 +120,7 @@ def test_random_batches_fresh_contexts(oracle_mod):
             reqs.append((m, lo, hi))
         exp = [tuple(oracle_mod.fast_scan_sum(m, lo, hi, threads=16)[0]) for m, lo, hi in reqs]
         with _lib.Context(devs) as c:
+            c.set_option(_lib.HM_OPT_FUSED, 0 if os.environ.get("HM_SOAK_FUSED", "1") == "0" else 1)
             c.set_option(_lib.HM_OPT_STREAMS, streams)
             c.set_option(_lib.HM_OPT_TABLE_ROWS_CAP, cap)
             got = c.scan_many(reqs)
