@@ -151,6 +151,113 @@ def shard_check(msg: bytes, lo, hi, res):
 
 
 SP_TIMEOUT_S = 180  # per single-process child (configs[3] on one GPU opened twice: ~60 s)
+# HIP streams per GPU of every hipminer context this bench opens (ranks and
+# single-process children; HM_OPT_STREAMS, made on first use since ABI 1.8):
+# each stream holds a hardware queue until its process exits, and the GPU
+# time-slices once the processes on it hold more than ~20 queues.
+# 2 = the dominant kernel's stream + one tail-filling stream.
+BENCH_STREAMS = int(os.environ.get("HM_BENCH_STREAMS", "2") or 2)
+KFD_PROC = "/sys/class/kfd/kfd/proc"
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpu_pci():
+    """KFD gpu_id -> PCI address ("dddd:bb:dd.f") from KFD's topology (sysfs;
+    no GPU call).  Empty when KFD is not visible."""
+    out = {}
+    try:
+        nodes = os.listdir(KFD_TOPOLOGY)
+    except OSError:
+        return out
+    for n in nodes:
+        try:
+            with open(os.path.join(KFD_TOPOLOGY, n, "gpu_id")) as f:
+                gid = f.read().strip()
+            props = {}
+            with open(os.path.join(KFD_TOPOLOGY, n, "properties")) as f:
+                for line in f:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+        except OSError:
+            continue
+        if gid in ("", "0") or "location_id" not in props:
+            continue
+        loc, dom = int(props["location_id"]), int(props.get("domain", "0"))
+        out[gid] = f"{dom:04x}:{loc >> 8:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7}"
+    return out
+
+
+def kfd_queues():
+    """User-mode (hardware) queues per GPU right now, over every process KFD
+    knows (/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/gpuid): {gpu_id:
+    {"queues": q, "processes": p}}, or {"error": ...} when KFD is not
+    readable.  Sysfs only, so it can run beside a GPU job."""
+    try:
+        pids = os.listdir(KFD_PROC)
+    except OSError as e:
+        return {"error": f"{KFD_PROC}: {type(e).__name__}"}
+    out = {}
+    for pid in pids:
+        qdir = os.path.join(KFD_PROC, pid, "queues")
+        try:
+            qids = os.listdir(qdir)
+        except OSError:
+            continue
+        seen = set()
+        for q in qids:
+            try:
+                with open(os.path.join(qdir, q, "gpuid")) as f:
+                    gid = f.read().strip()
+            except OSError:
+                continue
+            e = out.setdefault(gid, {"queues": 0, "processes": 0})
+            e["queues"] += 1
+            if gid not in seen:
+                seen.add(gid)
+                e["processes"] += 1
+    return out
+
+
+class QueueSampler:
+    """Samples kfd_queues() on a thread while a single-process child runs and
+    keeps each GPU's maximum: the queues and processes the GPUs actually
+    carried (the line recorded only a modelled process count)."""
+
+    def __init__(self, period_s: float = 0.25):
+        import threading
+        self.period_s, self.max, self.error, self.samples = period_s, {}, None, 0
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while True:
+            q = kfd_queues()
+            if "error" in q:
+                self.error = q["error"]
+            else:
+                self.samples += 1
+                for g, e in q.items():
+                    m = self.max.setdefault(g, {"queues": 0, "processes": 0})
+                    m["queues"] = max(m["queues"], e["queues"])
+                    m["processes"] = max(m["processes"], e["processes"])
+            if self._stop.wait(self.period_s):
+                return
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join(timeout=5)
+
+    def result(self) -> dict:
+        if self.error and not self.samples:
+            return {"error": self.error}
+        pci = kfd_gpu_pci()
+        return {"samples": self.samples, "period_s": self.period_s,
+                "max": {pci.get(g, f"gpu_id {g}"): v for g, v in sorted(self.max.items())},
+                "max_queues_any_gpu": max((v["queues"] for v in self.max.values()), default=0)}
 
 
 def single_process_cfg4(devices, rccl: bool):
@@ -166,6 +273,7 @@ def single_process_cfg4(devices, rccl: bool):
     merge_req = "rccl" if rccl else "host"
     try:
         with _lib.Context(devices) as c:
+            c.set_option(_lib.HM_OPT_STREAMS, BENCH_STREAMS)
             if rccl:
                 c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
             c.scan(m, 0, 10**9)  # module load, first launches, RCCL communicator
@@ -185,6 +293,7 @@ def single_process_cfg4(devices, rccl: bool):
             "kernel_GHs_per_device": round((hi + 1) / st["kernel_ms"] / 1e6, 3)
             if st["kernel_ms"] > 0 else None,
             "enqueue_ms": round(st["enqueue_ms"], 3), "mid_call_syncs": st["mid_call_syncs"],
+            "streams_per_gpu": BENCH_STREAMS,
             "result": {"hash": res[0], "nonce": res[1]},
             "result_vs_oracle": fixture_check(m, 0, hi, res)}
 
@@ -268,8 +377,12 @@ def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_
            "devices": list(devices), "timeout_s": timeout,
            "processes_per_gpu": {str(k): v for k, v in sorted(per_gpu.items())}}
     for merge, devs in (("host", list(devices)), ("rccl", rccl_devs)):
-        res = _run_child(child_cmd(merge, devs), timeout)
+        # the queues every process on each GPU holds while this child runs
+        # (KFD sysfs, sampled; keyed by PCI address)
+        with QueueSampler() as qs:
+            res = _run_child(child_cmd(merge, devs), timeout)
         res.setdefault("devices", devs)
+        res["queues_per_gpu"] = qs.result()
         out[merge] = res
     return out
 
@@ -444,15 +557,20 @@ def rounds_ops_per_nonce(seg, c_eff):
 
 def roofline(st, msg, lo, hi):
     """Roofline object of the dominant scan kernel of the last hm_scan (st =
-    hm_stats).  achieved = algorithmic ops per launch / average launch time
-    (HIP events on the launch stream).  `frac` prices the compressions per
-    nonce the kernel executes (dom_compressions_eff: the chained kernel of a
-    two-block tail hoists block 0 out of its loop, SURVEY §8(d) "fraction at
-    C = 1") at SURVEY's 1552 lane-ops each; `frac_algorithmic_C` prices
-    SURVEY's 1552*C with C counted before any hoisting (equal for one-block
-    tails); `frac_rounds` prices the rounds and schedule words the kernel's
-    formulation executes (rounds_ops_per_nonce: no credit for schedule work a
-    wave-uniform table or a hoist replaces)."""
+    hm_stats).  achieved = ops per launch / average launch time (HIP events
+    on the launch stream), with the ops priced per kernel kind (`pricing`):
+      tiled ("1552 x C"): SURVEY §8(d)'s 1552 lane-ops per compression x the
+        compressions per nonce the kernel runs (1, or 2 with a constant
+        trailer block; dom_compressions_eff);
+      chained ("rounds"): the rounds and schedule words the kernel's
+        formulation executes (rounds_ops_per_nonce) -- its final block's
+        schedule is a wave-uniform K+W table and block 0 is hoisted out of the
+        loop, so pricing either at 1552 lane-ops would credit work the kernel
+        never does (1552 x C_eff gave 0.97, 1552 x C 1.94).
+    `frac_algorithmic_C` always prices SURVEY's fixed 1552*C with C counted
+    before any hoisting (equal to `frac` for one-block tiled tails); for the
+    chained kernel it exceeds 1 by construction (block 0 once per ~1000
+    nonces).  `frac_rounds` is the rounds pricing for every kind."""
     from distributed_bitcoinminer_amd import _lib
     C = st["dom_compressions"]
     C_eff = st["dom_compressions_eff"] or C
@@ -484,9 +602,21 @@ def roofline(st, msg, lo, hi):
     tiles_pl = -(-int(nonces_pl) // 10 ** dom_seg["V"])
     algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
     tasks_pl = int(nonces_pl) // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
+    chained = dom_seg["kind"] == 3
+    if chained:  # priced by what the formulation executes (see docstring)
+        achieved, ops_pn, pricing = achieved_rounds, rops, "rounds"
+        note = (f"chained kernel: final-block schedule from a wave-uniform K+W table, block 0 "
+                f"hoisted (once per {1 / max(C_eff - 1, 1e-9):.0f} nonces): frac prices the "
+                f"executed rounds and schedule words; 1552 x C ({C}) would count "
+                f"{OPS_PER_COMPRESSION * C - rops:.0f} ops per nonce the kernel never runs")
+    else:
+        ops_pn, pricing = OPS_PER_COMPRESSION * C_eff, "1552 x C"
+        note = ("tiled kernel: SURVEY 8(d)'s 1552 lane-ops per compression x the "
+                "compressions per nonce it runs")
     return {"bound": "valu", "achieved": round(achieved, 3),
             "peak": round(PEAK_TOPS, 3), "unit": "T int32 lane-ops/s",
             "frac": round(achieved / PEAK_TOPS, 4),
+            "pricing": pricing, "pricing_note": note,
             "compressions_per_nonce": round(C_eff, 6),
             "frac_algorithmic_C": round(achieved_alg / PEAK_TOPS, 4),
             "compressions_per_nonce_algorithmic": C,
@@ -507,7 +637,7 @@ def roofline(st, msg, lo, hi):
             "launches_per_step": launches,
             "avg_launch_ms": round(avg_ms, 3),
             "nonces_per_launch": int(nonces_pl),
-            "ops_per_nonce": round(OPS_PER_COMPRESSION * C_eff, 3),
+            "ops_per_nonce": round(ops_pn, 3),
             "valu_instr_per_nonce_pmc": round(valu_pmc, 1) if valu_pmc else None,
             # executed lane-ops (PMC VALU instructions x 64 lanes per 64
             # nonces) / peak: the issue-level fraction
@@ -575,10 +705,10 @@ def main():
     from distributed_bitcoinminer_amd import build_id as bid
     build = {"build_id": _lib.build_id(), "build_matches_tree": _lib.build_id() == bid.tree_digest()}
     exit_code = 0
-    # HM_BENCH_STREAMS=1: strictly serial launches (kernel traces then
-    # attribute time without cross-stream queue waits)
-    if os.environ.get("HM_BENCH_STREAMS"):
-        ctx.set_option(_lib.HM_OPT_STREAMS, int(os.environ["HM_BENCH_STREAMS"]))
+    # BENCH_STREAMS (HM_BENCH_STREAMS, default 2) streams per GPU; 1 =
+    # strictly serial launches (kernel traces then attribute time without
+    # cross-stream queue waits)
+    ctx.set_option(_lib.HM_OPT_STREAMS, BENCH_STREAMS)
     dev = torch.device("cuda", gpu) if backend == "nccl" else torch.device("cpu")
     cdev = torch.device("cuda", gpu)
     cand = torch.empty(2, dtype=torch.int64, device=dev)
@@ -725,6 +855,16 @@ def main():
                 "all_ranks_match": all_match(rk2),
                 "roofline": roofline(st2, m2, lo2, hi2) if lo2 is not None else None}
 
+    # the hardware queues every process holds per GPU after the timed
+    # regions (each rank: torch + its communicator + BENCH_STREAMS hipminer
+    # streams), before any single-process child starts
+    queues_after = None
+    if rank == 0:
+        q = kfd_queues()
+        pci = kfd_gpu_pci()
+        queues_after = q if "error" in q else {pci.get(g, f"gpu_id {g}"): v
+                                               for g, v in sorted(q.items())}
+
     # configs[3] once more through SURVEY §8(e)'s single-process model, on a
     # multi-GPU run: rank 0 starts two child processes in turn (host merge,
     # RCCL merge), each driving every GPU through one hipminer context under
@@ -783,6 +923,7 @@ def main():
             "data": "synthetic (fixed message, contiguous nonce ranges; no dataset)",
             "config": {"workload": desc, "nonces_per_gpu": total_nonces // world,
                        "parallelism": f"dp{world} (nonce shards)",
+                       "hip_streams_per_gpu": BENCH_STREAMS,
                        "merge": ("RCCL all-gather" if backend == "nccl" else backend)
                                 if dist is not None else "none (1 rank)"},
             "result": {"hash": res[0], "nonce": res[1]},
@@ -795,6 +936,7 @@ def main():
         }
         if secondary:
             line["workloads"] = secondary
+        line["queues_per_gpu"] = queues_after
         if single is not None:
             line["single_process"] = single
         if world == 1 and not args.no_cpu_baseline:

@@ -23,6 +23,7 @@ HM_ERR_HIP = -3
 HM_ERR_NOMEM = -4
 HM_ERR_RCCL = -5
 HM_ERR_INTERNAL = -6
+HM_ERR_TIMEOUT = -7
 
 HM_KIND_NONE, HM_KIND_GENERIC, HM_KIND_TILED, HM_KIND_CHAINED, HM_KIND_FUSED = 0, 1, 2, 3, 4
 HM_OPT_FORCE_GENERIC, HM_OPT_MERGE_RCCL, HM_OPT_GRID_PER_CU, HM_OPT_STREAMS = 1, 2, 3, 4
@@ -32,6 +33,7 @@ HM_OPT_TEST_MID_SYNC = 9
 HM_OPT_FUSED = 10
 HM_OPT_FUSED_FLAGS = 11
 HM_OPT_FUSED_PARTS = 12
+HM_OPT_DEADLINE_MS = 13
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
@@ -60,7 +62,7 @@ class hm_stats(ctypes.Structure):
                 ("dom_launches", ctypes.c_int32), ("merge", ctypes.c_int32),
                 ("dom_kernel", ctypes.c_char * 64), ("dom_compressions_eff", ctypes.c_double),
                 ("enqueue_ms", ctypes.c_double), ("mid_call_syncs", ctypes.c_int32),
-                ("table_grows", ctypes.c_int32)]
+                ("table_grows", ctypes.c_int32), ("deadline_ms", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -126,6 +128,8 @@ def load() -> ctypes.CDLL:
         lib.hm_scan_cpu.restype = ctypes.c_int
         lib.hm_scan_cpu.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.POINTER(hm_result)]
+        lib.hm_debug_streams_made.restype = ctypes.c_int
+        lib.hm_debug_streams_made.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.hm_debug_plan.restype = ctypes.c_int
         lib.hm_debug_plan.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
@@ -204,6 +208,11 @@ class Context:
         if rc != HM_OK:
             raise HipMinerError(rc, "hm_scan_stats")
         return st.as_dict()
+
+    def streams_made(self, device_index: int = 0) -> int:
+        """HIP streams (hardware queues) the context has made on its
+        device_index-th device (debug export; ABI 1.8 makes them on first use)."""
+        return int(self._lib.hm_debug_streams_made(self._h, device_index))
 
     def set_option(self, opt: int, value: int) -> None:
         rc = self._lib.hm_set_option(self._h, opt, value)

@@ -28,6 +28,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hipminer.h"
@@ -89,12 +90,20 @@ void name_tiled(char* out, const SegPlan& s, bool csum) {
 struct Device {
     int ordinal = -1;
     int cus = 0;
+    int prio_hi = 0, prio_lo = 0;  // stream priorities (stream 0 / streams 1..)
+    // streams (and their buffers) made so far: stream 0 at hm_open, streams
+    // 1.. on the first call that enqueues onto them (make_streams).  Each HIP
+    // stream holds a hardware queue until the process exits, and the GPU
+    // time-slices once a process set holds more than ~20, so a
+    // context that only ever runs fused requests, or HM_OPT_STREAMS = 2,
+    // never creates the others.
+    int nmade = 0;
     hipStream_t stream[kStreams] = {};
     uint32_t* rec[kStreams] = {};
     uint32_t* kwt[kStreams] = {};
     uint32_t* aux[kStreams] = {};      // fused launches: s0 / trailer / K+W tables
     uint64_t kwt_rows[kStreams] = {};  // rows allocated (grown on demand, kw_table_rows)
-    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed after the call's waits
+    std::vector<uint32_t*> retired;    // tables replaced by larger ones, freed at hm_close
     uint64_t* cand[kStreams] = {};
     unsigned int* counter[kStreams] = {};
     uint64_t* sums[kStreams] = {};  // checked scans: per-wave (sum, count) slots
@@ -152,6 +161,16 @@ struct hm_ctx {
     int32_t table_grows = 0;
     double enqueue_ms = 0;
     bool csum = false;  // inside hm_scan_checked: checked kernels + coverage sums
+    // HM_OPT_DEADLINE_MS: 0 = none (the host blocks until the GPU is done),
+    // > 0 = that many ms per call, -1 = auto (deadline_for).  Past the
+    // deadline a call returns HM_ERR_TIMEOUT and the context is abandoned:
+    // its queued work may still run, so no later call touches its devices
+    // and hm_close leaks them rather than wait (SURVEY §8(b) liveness).
+    int64_t deadline_opt = 0;
+    bool has_deadline = false;
+    std::chrono::steady_clock::time_point deadline_at{};
+    double deadline_ms = 0;  // the current call's deadline (hm_stats.deadline_ms)
+    bool abandoned = false;
     bool have_stats = false;
     int merge = HM_MERGE_NONE;  // how the current call merged device results
     hm_stats last{};
@@ -169,21 +188,16 @@ int next_event(Device& dv, hipEvent_t* ev) {
     return HM_OK;
 }
 
-int device_init(Device& dv, int ordinal) {
-    dv.ordinal = ordinal;
-    HIPCHK(hipSetDevice(ordinal));
-    hipDeviceProp_t prop;
-    HIPCHK(hipGetDeviceProperties(&prop, ordinal));
-    dv.cus = prop.multiProcessorCount;
-    int prio_lo = 0, prio_hi = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    HIPCHK(hipModuleLoadData(&dv.mod, hm_scan_code_object));
-    for (int s = 0; s < kStreams; ++s) {
-        // stream 0 (the dominant kernel's segments) at the highest priority,
-        // the others at the lowest: their workgroups only fill what the
-        // dominant persistent launch leaves free, i.e. its tail
+// Create streams nmade..n-1 of dv and their per-stream buffers (device
+// current).  Stream 0 (the dominant kernel's segments, fused launches) runs
+// at the highest priority, the others at the lowest: their workgroups only
+// fill what the dominant persistent launch leaves free, i.e. its tail.
+// Neither hipStreamCreate nor hipMalloc waits for queued work, so a call may
+// make streams while it enqueues.
+int make_streams(Device& dv, int n) {
+    for (int s = dv.nmade; s < n && s < kStreams; ++s) {
         HIPCHK(hipStreamCreateWithPriority(&dv.stream[s], hipStreamNonBlocking,
-                                           s == 0 ? prio_hi : prio_lo));
+                                           s == 0 ? dv.prio_hi : dv.prio_lo));
         HIPCHK(hipMalloc(&dv.rec[s], (size_t)kMaxTilesPerLaunch * kRecWords * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&dv.cand[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipMalloc(&dv.kwt[s], (size_t)kMaxChainedTable * 64 * sizeof(uint32_t)));
@@ -192,7 +206,21 @@ int device_init(Device& dv, int ordinal) {
         HIPCHK(hipMalloc(&dv.counter[s], sizeof(unsigned int)));
         HIPCHK(hipMalloc(&dv.sums[s], (size_t)kMaxCandWaves * 2 * sizeof(uint64_t)));
         HIPCHK(hipEventCreateWithFlags(&dv.join[s], hipEventDisableTiming));
+        dv.nmade = s + 1;
     }
+    return HM_OK;
+}
+
+int device_init(Device& dv, int ordinal) {
+    dv.ordinal = ordinal;
+    HIPCHK(hipSetDevice(ordinal));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, ordinal));
+    dv.cus = prop.multiProcessorCount;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&dv.prio_lo, &dv.prio_hi));
+    HIPCHK(hipModuleLoadData(&dv.mod, hm_scan_code_object));
+    int rc = make_streams(dv, 1);
+    if (rc) return rc;
     HIPCHK(hipEventCreateWithFlags(&dv.gate, hipEventDisableTiming));
     HIPCHK(hipEventCreate(&dv.t0));
     HIPCHK(hipMalloc(&dv.best, (size_t)kMaxBatch * kStreams * 2 * sizeof(uint64_t)));
@@ -360,26 +388,49 @@ uint64_t tile_span_nonces(const SegPlan& s, uint64_t t, uint64_t nt) {
     return b - a + 1;
 }
 
-// The host-blocking HIP calls of a scan call -- a stream wait, a free (hipFree
-// waits for the whole device) and a synchronous readback -- go through these
-// three helpers and nowhere else (device_free at hm_close is outside any
-// call; tests/test_abi.py checks the sources for stray ones).  Each counts in
-// hm_stats.mid_call_syncs when the call is still enqueuing work (on this or a
-// later device): such a wait would hold back every launch after it.  No
-// enqueue path calls them (HM_OPT_TEST_MID_SYNC makes one, so tests can see
-// the counter work).  The enqueue path's only other host call that is not an
-// async launch, event record or memset is hipMalloc of a grown K+W table
-// (hm_stats.table_grows), which does not wait for queued work
-// (tests/test_gpu_enqueue.py bounds enqueue_ms against the call's wall).
+// The host-blocking HIP calls of a scan call -- a stream wait and a
+// synchronous readback -- go through these two helpers and nowhere else
+// (device_free at hm_close is outside any call; tests/test_abi.py checks the
+// sources for stray ones).  Each counts in hm_stats.mid_call_syncs when the
+// call is still enqueuing work (on this or a later device): such a wait would
+// hold back every launch after it.  No enqueue path calls them
+// (HM_OPT_TEST_MID_SYNC makes one, so tests can see the counter work).  The
+// enqueue path's only other host calls that are not async launches, event
+// records or memsets are hipMalloc of a grown K+W table (hm_stats.table_grows)
+// and of a context's streams 1.. on first use (make_streams), neither of
+// which waits for queued work (tests/test_gpu_enqueue.py bounds enqueue_ms
+// against the call's wall).  The library never calls hipFree during a call:
+// it waits for the whole device, other contexts' work included.
+//
+// With a deadline (HM_OPT_DEADLINE_MS) the stream wait polls hipStreamQuery
+// instead of blocking: spinning (yield) for the first 2 ms, then sleeping
+// 100 us between queries.  Past the deadline it abandons the context and
+// returns HM_ERR_TIMEOUT, so a hung or starved GPU scan cannot hold a miner
+// whose LSP thread keeps heartbeating (lsp_client.cpp) -- the server would
+// never reassign its chunk (server.go:326-376).
 int host_wait(hm_ctx* ctx, hipStream_t st) {
     if (ctx->enqueuing) ++ctx->mid_syncs;
-    HIPCHK(hipStreamSynchronize(st));
-    return HM_OK;
-}
-int host_free(hm_ctx* ctx, void* p) {
-    if (ctx->enqueuing) ++ctx->mid_syncs;
-    HIPCHK(hipFree(p));
-    return HM_OK;
+    if (!ctx->has_deadline) {
+        HIPCHK(hipStreamSynchronize(st));
+        return HM_OK;
+    }
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e == hipSuccess) return HM_OK;
+        if (e != hipErrorNotReady) return hip_fail(e, "hipStreamQuery");
+        const auto now = clk::now();
+        if (now >= ctx->deadline_at) {
+            ctx->abandoned = true;
+            if (debug_on())
+                fprintf(stderr, "hipminer: scan deadline of %.1f ms passed: context abandoned\n",
+                        ctx->deadline_ms);
+            return HM_ERR_TIMEOUT;
+        }
+        if (now - t0 < std::chrono::milliseconds(2)) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
 }
 int host_read(hm_ctx* ctx, void* dst, const void* src, size_t n) {
     if (ctx->enqueuing) ++ctx->mid_syncs;
@@ -390,11 +441,10 @@ int host_read(hm_ctx* ctx, void* dst, const void* src, size_t n) {
 // Make stream si's K+W table hold `rows` rows.  Grown once to the largest
 // table used so far (10^5 .. 10^7 rows, up to 2.56 GB, for final blocks of
 // >= 5 digits).  Work queued earlier on the stream may still read the old
-// table, and hipFree would wait for the device, so mid-enqueue the old
-// table is only retired; free_retired releases it at the end of the call,
-// once the host has waited for all of the call's work.  Peak device memory
-// during a growing call: the old and the new table (rows are powers of ten,
-// so the old one holds < 1/9 of the new one, at most 0.28 GB).
+// table, and hipFree would wait for the whole device (other contexts' work
+// too), so the old table is retired and freed at hm_close.  Rows are powers
+// of ten, so all tables a stream retires together hold < 1/9 of its current
+// one (at most 0.28 GB beside a 2.56-GB table).
 // Returns HM_ERR_NOMEM (with HIP's error state cleared, the old table kept)
 // when the device cannot hold the table, or the HM_OPT_TABLE_ROWS_CAP test
 // hook refuses it; the caller then plans smaller tables.
@@ -410,22 +460,6 @@ int kw_table_rows(hm_ctx* ctx, Device& dv, int si, uint64_t rows) {
     dv.kwt[si] = t;
     dv.kwt_rows[si] = rows;
     ++ctx->table_grows;
-    return HM_OK;
-}
-
-// Free the K+W tables retired by kw_table_rows during the call.  Called after
-// the host has waited for every device's stream 0, which joins all of the
-// device's streams: no queued work can still read them.
-int free_retired(hm_ctx* ctx) {
-    for (auto& dv : ctx->devs) {
-        if (dv.retired.empty()) continue;
-        HIPCHK(hipSetDevice(dv.ordinal));
-        for (uint32_t* t : dv.retired) {
-            int rc = host_free(ctx, t);
-            if (rc) return rc;
-        }
-        dv.retired.clear();
-    }
     return HM_OK;
 }
 
@@ -854,15 +888,6 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
                                                ctx->force_generic, ctx->table_digits);
         if (fusible(segs)) return enqueue_fused(ctx, dv, *reqs[0].mp, segs, 0, dv.result, true);
     }
-    HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
-    HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
-    if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
-    HIPCHK(hipEventRecord(dv.join[0], s0));
-    for (int s = 1; s < kStreams; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
-    if (ctx->test_mid_sync) {  // HM_OPT_TEST_MID_SYNC: a host wait mid-enqueue, counted
-        int rc = host_wait(ctx, s0);
-        if (rc) return rc;
-    }
     // streams == 1: every segment in order on stream 0, so kernels never
     // overlap and per-kernel timings match rocprofv3 exactly.  streams > 1:
     // the segments run by the request's dominant kernel instantiation (most
@@ -873,38 +898,77 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     // tail instead of after it.  Small requests (<= kConcurrentNonces) skip
     // that order: all their segments run at once on all streams.
     const int nstreams = std::max(1, std::min(ctx->streams, kStreams));
-    int rr = 0;
+    // instantiation key per segment
+    auto key = [](const SegPlan& g) {
+        return g.kind * 1000 + g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0);
+    };
+    struct ReqPlan {
+        std::vector<SegPlan> segs;
+        int dom = -1;            // the key with the most nonces
+        long double total = 0;   // nonces
+        bool fused = false;
+    };
+    // plan every request first: the streams the batch needs are made (once
+    // per context, make_streams) before anything is queued on them
+    std::vector<ReqPlan> plans(n);
+    int used = 1, nfused = 0;
     for (int r = 0; r < n; ++r) {
         if (reqs[r].empty) continue;
-        std::vector<SegPlan> segs = plan_range(*reqs[r].mp, reqs[r].lo, reqs[r].hi,
-                                               ctx->force_generic, ctx->table_digits);
-        // instantiation key per segment, and the key with the most nonces
-        auto key = [](const SegPlan& g) {
-            return g.kind * 1000 + g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0);
-        };
+        ReqPlan& P = plans[r];
+        P.segs = plan_range(*reqs[r].mp, reqs[r].lo, reqs[r].hi, ctx->force_generic,
+                            ctx->table_digits);
         std::vector<std::pair<int, long double>> load;
-        for (const auto& g : segs) {
+        for (const auto& g : P.segs) {
             const long double cnt = (long double)(g.hi - g.lo) + 1;
             auto it = std::find_if(load.begin(), load.end(),
                                    [&](const auto& p) { return p.first == key(g); });
             if (it == load.end()) load.push_back({key(g), cnt});
             else it->second += cnt;
         }
-        int dom = load.empty() ? -1 : load[0].first;
-        long double most = -1, total = 0;
+        long double most = -1;
         for (const auto& p : load) {
-            total += p.second;
-            if (p.second > most) { most = p.second; dom = p.first; }
+            P.total += p.second;
+            if (p.second > most) { most = p.second; P.dom = p.first; }
         }
+        P.fused = ctx->fused && fusible(P.segs);
+        if (P.fused) {
+            used = std::max(used, std::min(nstreams, ++nfused));
+        } else if (P.total <= (long double)kConcurrentNonces) {
+            used = std::max(used, std::min(nstreams, (int)P.segs.size()));
+        } else {
+            int off = 0;  // segments off the dominant key: the tail streams
+            for (const auto& g : P.segs) off += key(g) != P.dom;
+            used = std::max(used, std::min(nstreams, 1 + off));
+        }
+    }
+    const int ns = used;  // streams this batch enqueues onto (<= nstreams)
+    {
+        int rc = make_streams(dv, ns);
+        if (rc) return rc;
+    }
+    HIPCHK(launch_init_best(dv.best, (uint32_t)(n * kStreams), s0));
+    HIPCHK(launch_init_best(dv.result, (uint32_t)n, s0));
+    if (ctx->csum) HIPCHK(hipMemsetAsync(dv.acc, 0, kStreams * 2 * sizeof(uint64_t), s0));
+    HIPCHK(hipEventRecord(dv.join[0], s0));
+    for (int s = 1; s < ns; ++s) HIPCHK(hipStreamWaitEvent(dv.stream[s], dv.join[0], 0));
+    if (ctx->test_mid_sync) {  // HM_OPT_TEST_MID_SYNC: a host wait mid-enqueue, counted
+        int rc = host_wait(ctx, s0);
+        if (rc) return rc;
+    }
+    int rr = 0;
+    for (int r = 0; r < n; ++r) {
+        if (reqs[r].empty) continue;
+        const std::vector<SegPlan>& segs = plans[r].segs;
+        const int dom = plans[r].dom;
         uint64_t* best = dv.best + (size_t)r * kStreams * 2;
-        if (ctx->fused && fusible(segs)) {
+        if (plans[r].fused) {
             // a small request of a batch: one fused launch on the next stream
-            const int si = rr++ % nstreams;
+            const int si = rr++ % ns;
             int rc = enqueue_fused(ctx, dv, *reqs[r].mp, segs, si, best + 2 * si, false);
             if (rc) return rc;
             continue;
         }
-        if (nstreams > 1 && total <= (long double)kConcurrentNonces) {
+        if (ns > 1 && plans[r].total <= (long double)kConcurrentNonces) {
             // a small request (config 1's [0, 10^7+1], short server chunks):
             // its launches are latency-bound, so every segment goes onto the
             // streams round-robin, ungated, largest first: the host enqueues
@@ -916,7 +980,7 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
                 return segs[a].hi - segs[a].lo > segs[b].hi - segs[b].lo;
             });
             for (size_t i : order) {
-                int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], rr++ % nstreams, best);
+                int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], rr++ % ns, best);
                 if (rc) return rc;
             }
             continue;
@@ -924,16 +988,16 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
         size_t last_dom = 0;
         for (size_t i = 0; i < segs.size(); ++i)
             if (key(segs[i]) == dom) last_dom = i;
-        for (int pass = 0; pass < (nstreams > 1 ? 2 : 1); ++pass) {
+        for (int pass = 0; pass < (ns > 1 ? 2 : 1); ++pass) {
             if (pass == 1)
-                for (int q = 1; q < nstreams; ++q)
+                for (int q = 1; q < ns; ++q)
                     HIPCHK(hipStreamWaitEvent(dv.stream[q], dv.gate, 0));
             for (size_t i = 0; i < segs.size(); ++i) {
                 int si = 0;
-                if (nstreams > 1) {
+                if (ns > 1) {
                     const bool is_dom = key(segs[i]) == dom;
                     if (is_dom != (pass == 0)) continue;
-                    if (!is_dom) si = 1 + (rr++ % (nstreams - 1));
+                    if (!is_dom) si = 1 + (rr++ % (ns - 1));
                     if (is_dom && i == last_dom) HIPCHK(hipEventRecord(dv.gate, dv.stream[0]));
                 }
                 int rc = enqueue_segment(ctx, dv, *reqs[r].mp, segs[i], si, best);
@@ -941,7 +1005,7 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
             }
         }
     }
-    for (int s = 1; s < kStreams; ++s) {
+    for (int s = 1; s < ns; ++s) {
         HIPCHK(hipEventRecord(dv.join[s], dv.stream[s]));
         HIPCHK(hipStreamWaitEvent(s0, dv.join[s], 0));
     }
@@ -1046,7 +1110,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
             if (rc) return rc;
         }
         for (int r = 0; r < nreq; ++r) outs[r] = d0.host_out[r];
-        return free_retired(ctx);
+        return HM_OK;
     }
     ctx->merge = ndev > 1 ? HM_MERGE_HOST : HM_MERGE_NONE;
     for (auto& dv : ctx->devs) {
@@ -1063,7 +1127,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
             if (lex_less(dv.host_out[r].hash, dv.host_out[r].nonce, outs[r].hash, outs[r].nonce))
                 outs[r] = dv.host_out[r];
     }
-    return free_retired(ctx);
+    return HM_OK;
 }
 
 int open_devices(const int* devices, int ndev, hm_ctx** out);
@@ -1081,8 +1145,10 @@ uint64_t hm_hash(const uint8_t* msg, size_t len, uint64_t nonce) {
 // 1.4: hm_stats.merge / dom_compressions_eff, HM_OPT_MERGE_RCCL at any device count;
 // 1.5: hm_scan_stats_sized, HM_OPT_MERGE_RCCL refused up front for repeated ordinals;
 // 1.6: hm_build_id, hm_stats.enqueue_ms / mid_call_syncs / table_grows, HM_OPT_TABLE_ROWS_CAP;
-// 1.7: hm_scan_cpu, hm_scan_stats frozen at HM_STATS_SIZE_1_4 bytes
-int hm_version(void) { return (1 << 16) | 7; }
+// 1.7: hm_scan_cpu, hm_scan_stats frozen at HM_STATS_SIZE_1_4 bytes;
+// 1.8: HM_OPT_DEADLINE_MS / HM_ERR_TIMEOUT, hm_stats.deadline_ms, streams 1..
+//      made on first use
+int hm_version(void) { return (1 << 16) | 8; }
 
 // The digest of the sources this library was built from (build_id.py), kept
 // in the binary behind a tag so tools can read it without loading the library.
@@ -1113,6 +1179,9 @@ const char* hm_strerror(int rc) {
         case HM_ERR_NOMEM: return "out of memory";
         case HM_ERR_RCCL: return "RCCL error";
         case HM_ERR_INTERNAL: return "internal planner error";
+        case HM_ERR_TIMEOUT:
+            return "GPU scan missed its deadline (HM_OPT_DEADLINE_MS); the context is "
+                   "abandoned: close it, open a new one or scan on the host";
         default: return "unknown error";
     }
 }
@@ -1165,7 +1234,11 @@ void hm_close(hm_ctx* ctx) {
     if (!ctx) return;
     {
         std::lock_guard<std::mutex> g(ctx->mu);
-        for (auto& dv : ctx->devs) device_free(dv);
+        // an abandoned context (HM_ERR_TIMEOUT) may still have work running:
+        // its streams, buffers and pinned readback slot are left to the
+        // process exit rather than waited for
+        if (!ctx->abandoned)
+            for (auto& dv : ctx->devs) device_free(dv);
     }
     delete ctx;
 }
@@ -1173,7 +1246,12 @@ void hm_close(hm_ctx* ctx) {
 int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
     if (!ctx) return HM_ERR_INVALID;
     std::lock_guard<std::mutex> g(ctx->mu);
+    if (ctx->abandoned) return HM_ERR_TIMEOUT;
     switch (opt) {
+        case HM_OPT_DEADLINE_MS:
+            if (value < -1) return HM_ERR_INVALID;
+            ctx->deadline_opt = value;
+            return HM_OK;
         case HM_OPT_FORCE_GENERIC: ctx->force_generic = value != 0; return HM_OK;
         case HM_OPT_MERGE_RCCL:
             // RCCL needs one rank per device: a context naming a device twice
@@ -1219,9 +1297,46 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
 
 namespace {
 
+// HM_OPT_DEADLINE_MS = -1 (auto): kDeadlineFloorMs plus kDeadlineSlack times
+// the call's modelled kernel time -- every segment's nonces at its layout's
+// measured SIMD cycles per 64 nonces (seg_cost, the model hm_partition
+// balances shards with), over every SIMD of the context's distinct devices at
+// the nominal 2.4 GHz.  The slack covers a GPU shared with other processes,
+// a lowered clock and the fused launch's partial grid; hm_miner and the Go
+// gpuminer use it so a hung or starved GPU scan is answered on the host
+//  long before any healthy scan could finish that late.
+constexpr double kDeadlineFloorMs = 2000.0;
+constexpr double kDeadlineSlack = 8.0;
+
+double auto_deadline_ms(const hm_ctx* ctx, const hm_request* reqs, int n) {
+    static const uint8_t empty_msg = 0;
+    long double cycles = 0;
+    for (int r = 0; r < n; ++r) {
+        const hm_request& q = reqs[r];
+        if (q.lo > q.hi) continue;
+        const MsgPlan mp = plan_message(q.msg ? q.msg : &empty_msg, q.msg ? q.len : 0);
+        for (const SegPlan& g : plan_range(mp, q.lo, q.hi, ctx->force_generic, ctx->table_digits))
+            cycles += ((long double)(g.hi - g.lo) + 1) * seg_cost(g) / kWaveSize;
+    }
+    std::vector<int> ords;
+    for (const auto& dv : ctx->devs)
+        if (std::find(ords.begin(), ords.end(), dv.ordinal) == ords.end()) ords.push_back(dv.ordinal);
+    const long double simds = 4.0L * ctx->devs[0].cus * (long double)ords.size();
+    return kDeadlineFloorMs + kDeadlineSlack * (double)(cycles / simds / 2.4e6L);
+}
+
 // hm_scan_many with ctx->mu held.
 int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs) {
     const auto t0 = std::chrono::steady_clock::now();
+    // an abandoned context's devices may still run its timed-out work
+    if (ctx->abandoned) return HM_ERR_TIMEOUT;
+    ctx->has_deadline = ctx->deadline_opt != 0;
+    ctx->deadline_ms = !ctx->has_deadline ? 0.0
+                       : ctx->deadline_opt > 0 ? (double)ctx->deadline_opt
+                                               : auto_deadline_ms(ctx, reqs, n);
+    if (ctx->has_deadline)
+        ctx->deadline_at = t0 + std::chrono::duration_cast<std::chrono::steady_clock::duration>(
+                                    std::chrono::duration<double, std::milli>(ctx->deadline_ms));
     std::vector<hm_result> res(n);
     for (auto& dv : ctx->devs) {
         dv.evnext = 0;
@@ -1305,6 +1420,7 @@ int scan_many_locked(hm_ctx* ctx, const hm_request* reqs, int n, hm_result* outs
     st.enqueue_ms = ctx->enqueue_ms;
     st.mid_call_syncs = ctx->mid_syncs;
     st.table_grows = ctx->table_grows;
+    st.deadline_ms = ctx->deadline_ms;
     st.wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
                      .count();
     ctx->last = st;
@@ -1379,6 +1495,15 @@ int hm_scan_stats_sized(const hm_ctx* ctx, hm_stats* out, size_t size) {
 size_t hm_debug_code_object(const unsigned char** p) {
     if (p) *p = hm_scan_code_object;
     return (size_t)(hm_scan_code_object_end - hm_scan_code_object);
+}
+
+// Streams (hardware queues) made so far on device i of ctx (make_streams):
+// 1 after hm_open, up to HM_OPT_STREAMS once calls used them; -1 if i is out
+// of range.
+int hm_debug_streams_made(const hm_ctx* ctx, int i) {
+    if (!ctx || i < 0 || i >= (int)ctx->devs.size()) return -1;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    return ctx->devs[i].nmade;
 }
 
 // Writes up to `cap` segment descriptors as 13 x int64:

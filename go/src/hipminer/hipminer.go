@@ -40,7 +40,14 @@ func cbytes(s string) *C.uint8_t {
 const (
 	ErrInvalid  = int(C.HM_ERR_INVALID)
 	ErrNoDevice = int(C.HM_ERR_NO_DEVICE)
+	// ErrTimeout (ABI 1.8): the scan missed its deadline (SetDeadline); the
+	// context is abandoned -- Close it (no device wait) and answer elsewhere.
+	ErrTimeout = int(C.HM_ERR_TIMEOUT)
 )
+
+// DeadlineAuto makes SetDeadline use the library's modelled deadline: 2 s +
+// 8x the call's modelled kernel time.
+const DeadlineAuto = -1
 
 // Error carries an hm_* return code.
 type Error struct{ Code int }
@@ -71,6 +78,17 @@ func Open(devices ...int) (*Miner, error) {
 		return nil, Error{int(rc)}
 	}
 	return &Miner{ctx: ctx}, nil
+}
+
+// SetDeadline bounds every later scan on m (HM_OPT_DEADLINE_MS): ms > 0 that
+// many milliseconds per call, DeadlineAuto the modelled deadline, 0 none.  A
+// scan past its deadline returns Error{ErrTimeout} instead of blocking, so a
+// hung GPU cannot keep a heartbeating miner from answering (SURVEY §8(b)).
+func (m *Miner) SetDeadline(ms int64) error {
+	if rc := C.hm_set_option(m.ctx, C.HM_OPT_DEADLINE_MS, C.int64_t(ms)); rc != 0 {
+		return Error{int(rc)}
+	}
+	return nil
 }
 
 // ScanInclusive returns the lexicographic min of (Hash(data, n), n) over the
@@ -151,9 +169,10 @@ func (m *Miner) EvalRequest(data string, lower, upper uint64) (hash, nonce uint6
 }
 
 // ScanCPU is hm_scan_cpu: the same scan as ScanInclusive, bit-identical, on
-// the host's cores (threads <= 0: every hardware thread).  For a miner whose
-// GPU is missing or failed, so that a Result is still written (SURVEY
-// §8(b)); orders of magnitude slower than the GPU.
+// the host's cores (threads <= 0: one thread per CPU in this process's
+// affinity mask, at most 1024 -- not every hardware thread of the machine).
+// For a miner whose GPU is missing or failed, so that a Result is still
+// written (SURVEY §8(b)); orders of magnitude slower than the GPU.
 func ScanCPU(data string, lo, hi uint64, threads int) (hash, nonce uint64, err error) {
 	var out C.hm_result
 	p := cbytes(data)
@@ -175,7 +194,8 @@ func EvalRequestCPU(data string, lower, upper uint64, threads int) (hash, nonce 
 	return ScanCPU(data, lower, end-1, threads)
 }
 
-// Close releases the context.
+// Close releases the context (an abandoned one after ErrTimeout: host
+// memory only, without waiting on the device).
 func (m *Miner) Close() {
 	if m.ctx != nil {
 		C.hm_close(m.ctx)

@@ -38,7 +38,8 @@
  *
  * Errors: 0 = HM_OK; negative codes below; hm_strerror() describes them.
  * Nothing aborts the process, and a failed GPU scan is reported, never
- * silently replaced.  hm_scan_cpu (ABI 1.7) is the host scan a caller may
+ * silently replaced.  With HM_OPT_DEADLINE_MS a scan that the GPU does not
+ * finish in time returns HM_ERR_TIMEOUT instead of blocking (ABI 1.8).  hm_scan_cpu (ABI 1.7) is the host scan a caller may
  * choose when hm_open or hm_scan fails, so that a Result is still written
  * (SURVEY §8(b)); the GPU entry points never call it.
  */
@@ -106,17 +107,21 @@ typedef struct hm_stats {
                                 host waits on any, so devices overlap)          */
     int32_t table_grows;     /* chained K+W tables enlarged by the call; an old
                                 table may still be read by queued work, so it
-                                is kept (< 1/9 of the new one) until the call
-                                has waited for its work and freed then (ABI
-                                1.7; 1.6 kept it until hm_close): growth never
-                                waits on the device mid-enqueue (ABI 1.6)     */
+                                is kept (< 1/9 of the new one) until
+                                hm_close, as hipFree would wait for the whole
+                                device (1.7 freed it at the end of the call):
+                                growth never waits on the device mid-enqueue
+                                (ABI 1.6)                                       */
+    double deadline_ms;      /* the deadline the call ran under (ABI 1.8;
+                                HM_OPT_DEADLINE_MS; 0 = none)                    */
 } hm_stats;
 
 /* sizeof(hm_stats) by ABI version.  The struct only grows at its end. */
 #define HM_STATS_SIZE_1_0 136 /* ABI 1.0 .. 1.3                                 */
 #define HM_STATS_SIZE_1_4 144 /* ABI 1.4, 1.5: + dom_compressions_eff          */
-#define HM_STATS_SIZE_1_6 160 /* ABI 1.6+: + enqueue_ms, mid_call_syncs,
+#define HM_STATS_SIZE_1_6 160 /* ABI 1.6, 1.7: + enqueue_ms, mid_call_syncs,
                                  table_grows                                     */
+#define HM_STATS_SIZE_1_8 168 /* ABI 1.8+: + deadline_ms                         */
 
 #define HM_MERGE_NONE 0 /* one device: its result is read back directly      */
 #define HM_MERGE_HOST 1 /* several devices: 16-B results merged on the host  */
@@ -131,6 +136,15 @@ typedef struct hm_stats {
 #define HM_ERR_NOMEM (-4)     /* device or host allocation failed                */
 #define HM_ERR_RCCL (-5)      /* an RCCL call failed                              */
 #define HM_ERR_INTERNAL (-6)  /* planner invariant violated                      */
+#define HM_ERR_TIMEOUT (-7)   /* ABI 1.8: the call passed its HM_OPT_DEADLINE_MS
+                                 deadline before the GPU finished.  The context
+                                 is ABANDONED: its queued work may still run, so
+                                 every later call on it returns HM_ERR_TIMEOUT
+                                 without touching a device, and hm_close frees
+                                 only host memory (device buffers and streams
+                                 are left to the process exit).  `out` is not
+                                 written: the caller answers from hm_scan_cpu or
+                                 a new context.                                  */
 
 #define HM_KIND_NONE 0
 #define HM_KIND_GENERIC 1  /* one nonce per lane, generic tail builder          */
@@ -151,7 +165,12 @@ typedef struct hm_stats {
                                   (1..4, default 4): the dominant kernel's
                                   segments on a high-priority stream, the
                                   others on low-priority streams that fill
-                                  its last launch's tail; 1 = strictly serial */
+                                  its last launch's tail; 1 = strictly serial.
+                                  Since ABI 1.8 hm_open makes stream 0 only and
+                                  a call makes streams 1.. when it first
+                                  enqueues onto them: every HIP stream holds a
+                                  hardware queue until the process exits, so a
+                                  process sharing its GPU sets 1 or 2        */
 #define HM_OPT_TABLE_DIGITS 7  /* test hook (-1..7, 0 = default 7): the final-
                                   block digits one K+W table of the chained
                                   kernel covers; the remaining high final-block
@@ -185,6 +204,18 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */
+#define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
+                                  a call blocks until its GPU work is done; > 0 =
+                                  a call returns HM_ERR_TIMEOUT (and abandons the
+                                  context) once this many ms have passed since it
+                                  began; -1 = auto: 2 s + 8 x the call's modelled
+                                  kernel time (the layouts' measured cost, the
+                                  model hm_partition balances with).  The host
+                                  then polls the GPU instead of blocking on it.
+                                  A miner whose LSP thread keeps heartbeating
+                                  would otherwise hold its chunk forever: the
+                                  server reassigns only dropped miners
+                                  (server.go:326-376)                           */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */
@@ -244,7 +275,11 @@ int hm_partition(const uint8_t *msg, size_t len, uint64_t lo, uint64_t hi, int n
  * ABI 1.4/1.5 headers promised.  Frozen since ABI 1.7, so a binary built
  * against any header from 1.4 on never gets more bytes than its struct
  * holds (ABI 1.6 wrote 160 bytes here, past a 1.5 caller's struct).  The
- * fields after dom_compressions_eff come only from hm_scan_stats_sized. */
+ * fields after dom_compressions_eff come only from hm_scan_stats_sized.
+ * A caller built against the 1.6 header that reads enqueue_ms,
+ * mid_call_syncs or table_grows MUST switch to hm_scan_stats_sized (pass
+ * sizeof(hm_stats)): through this export those fields are no longer
+ * written and hold whatever the caller's struct held. */
 int hm_scan_stats(const hm_ctx *ctx, hm_stats *out);
 
 /* hm_scan_stats writing at most `size` bytes (pass sizeof(hm_stats) as the

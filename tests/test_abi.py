@@ -27,10 +27,24 @@ def test_library_is_gfx950_code_object():
 def test_version_and_strerror():
     lib = _lib.load()
     assert lib.hm_version() >> 16 == 1
-    assert lib.hm_version() & 0xFFFF >= 7  # 1.7: hm_scan_cpu, hm_scan_stats frozen at 144 B
-    for rc in range(0, -7, -1):
-        assert _lib.strerror(rc)
+    assert lib.hm_version() & 0xFFFF >= 8  # 1.8: HM_OPT_DEADLINE_MS / HM_ERR_TIMEOUT
+    for rc in range(0, -8, -1):
+        assert _lib.strerror(rc) != "unknown error", rc
     assert _lib.strerror(-99) == "unknown error"
+    assert "deadline" in _lib.strerror(_lib.HM_ERR_TIMEOUT)
+
+
+def test_timeout_code_and_deadline_option_in_header():
+    """ABI 1.8 (SURVEY §8(b) liveness): the header defines HM_ERR_TIMEOUT and
+    HM_OPT_DEADLINE_MS with the values the bindings use (ctypes, cgo via the
+    header itself), and hm_set_option checks the option's range."""
+    import re
+    text = open(_lib.HEADER_PATH).read()
+    assert int(re.search(r"#define HM_ERR_TIMEOUT \((-?\d+)\)", text).group(1)) == \
+        _lib.HM_ERR_TIMEOUT == -7
+    assert int(re.search(r"#define HM_OPT_DEADLINE_MS (\d+)", text).group(1)) == \
+        _lib.HM_OPT_DEADLINE_MS == 13
+    assert _lib.load().hm_set_option(None, _lib.HM_OPT_DEADLINE_MS, 5) == _lib.HM_ERR_INVALID
 
 
 def test_hm_hash_matches_golden(golden):
@@ -81,23 +95,25 @@ def test_struct_layouts_match_header(tmp_path):
 def test_stats_size_is_pinned(tmp_path):
     """hm_stats only grows at its end: the 1.0-1.3 callers' 136-byte struct is
     the prefix before dom_compressions_eff, the 1.4/1.5 struct the 144 bytes
-    before enqueue_ms, the 1.6 struct is 160 bytes, and hm_scan_stats_sized
-    refuses a size below the oldest layout."""
+    before enqueue_ms, the 1.6/1.7 struct is 160 bytes, the 1.8 struct 168
+    (+ deadline_ms), and hm_scan_stats_sized refuses a size below the oldest
+    layout."""
     import subprocess
     src = tmp_path / "sz.c"
     src.write_text("\n".join([
         '#include <stddef.h>', '#include <stdio.h>', f'#include "{_lib.HEADER_PATH}"',
         "int main(void) {",
-        '  printf("%zu %zu %zu %d %d %d\\n", sizeof(hm_stats),',
+        '  printf("%zu %zu %zu %zu %d %d %d %d\\n", sizeof(hm_stats),',
         "         offsetof(hm_stats, dom_compressions_eff), offsetof(hm_stats, enqueue_ms),",
-        "         HM_STATS_SIZE_1_0, HM_STATS_SIZE_1_4, HM_STATS_SIZE_1_6);",
+        "         offsetof(hm_stats, deadline_ms),",
+        "         HM_STATS_SIZE_1_0, HM_STATS_SIZE_1_4, HM_STATS_SIZE_1_6, HM_STATS_SIZE_1_8);",
         "  return 0;", "}"]))
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
     out = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True,
                                           text=True).stdout.split()]
-    assert out == [160, 136, 144, 136, 144, 160]
-    assert ctypes.sizeof(_lib.hm_stats) == 160
+    assert out == [168, 136, 144, 160, 136, 144, 160, 168]
+    assert ctypes.sizeof(_lib.hm_stats) == 168
     lib = _lib.load()
     st = _lib.hm_stats()
     assert lib.hm_scan_stats_sized(None, ctypes.byref(st), 144) == _lib.HM_ERR_INVALID
@@ -174,14 +190,16 @@ def test_host_blocking_calls_only_in_counting_helpers():
     """hm_stats.mid_call_syncs counts host waits issued while a call is still
     enqueuing.  That holds by construction only if every host-blocking HIP
     call of the library (stream/device/event waits, hipFree, synchronous
-    hipMemcpy) sits in the counting helpers host_wait / host_free / host_read,
-    or in device_free (hm_close, outside any call).  Scan every C++ source of
-    the library for stray ones."""
+    hipMemcpy) sits in the counting helpers host_wait / host_read, or in
+    device_free (hm_close, outside any call).  Since ABI 1.8 no call frees
+    device memory at all (hipFree waits for the whole device, other
+    contexts' work included).  Scan every C++ source of the library for
+    stray ones."""
     import re
     csrc = os.path.join(os.path.dirname(_lib.__file__), "csrc")
     blocking = re.compile(r"\b(hipStreamSynchronize|hipDeviceSynchronize|hipEventSynchronize|"
                           r"hipFree|hipMemcpy)\s*\(")
-    allowed = {"host_wait", "host_free", "host_read", "device_free"}
+    allowed = {"host_wait", "host_read", "device_free"}
     func = re.compile(r"^[A-Za-z_][\w:<>*& ]*?\b(\w+)\s*\([^;]*\)\s*(const\s*)?\{\s*$")
     stray = []
     for name in sorted(os.listdir(csrc)):

@@ -50,9 +50,10 @@ def test_profiled_requires_this_code_object(tmp_path, monkeypatch):
     assert bench.profiled("k")[:3] == (1.0, 2.3, 1200.0)
 
 
-def test_roofline_prices_executed_compressions(monkeypatch):
-    """frac uses C_eff (compressions the kernel executes per nonce), the
-    algorithmic 1552*C is reported beside it."""
+def test_roofline_prices_the_chained_kernel_by_rounds(monkeypatch):
+    """the chained kernel's frac prices the rounds and schedule
+    words it executes (frac == frac_rounds), not 1552 x C_eff; SURVEY's
+    1552*C figure stays as frac_algorithmic_C (> 1 by the hoist)."""
     from distributed_bitcoinminer_amd import _lib
     monkeypatch.setattr(bench, "profiled", lambda k: (None, None, None, None))
     st = {"dom_compressions": 2, "dom_compressions_eff": 1.001, "dom_launches": 3,
@@ -60,7 +61,9 @@ def test_roofline_prices_executed_compressions(monkeypatch):
           "dom_kernel": "hm_chained_kernel"}
     rl = bench.roofline(st, bench.long120(), 0, 2**32 - 1)
     ghs = 4_284_967_296 / 0.09
-    assert abs(rl["frac"] - ghs * 1552 * 1.001 / 78.6432e12) < 1e-3
+    assert rl["pricing"] == "rounds" and rl["frac"] == rl["frac_rounds"]
+    assert abs(rl["ops_per_nonce"] - rl["ops_per_nonce_rounds"]) < 0.01
+    assert "hoisted" in rl["pricing_note"]
     assert abs(rl["frac_algorithmic_C"] - ghs * 1552 * 2 / 78.6432e12) < 1e-3
     assert rl["compressions_per_nonce"] == 1.001 and rl["compressions_per_nonce_algorithmic"] == 2
     assert _lib.debug_plan(bench.long120(), 0, 2**32 - 1)  # the plan the line reads
@@ -71,6 +74,22 @@ def test_roofline_prices_executed_compressions(monkeypatch):
     ops = 1024 + 1552 * 0.001 + sum(10 ** s["f"] * (48 * 11 + 64) for s in segs) / n
     assert abs(rl["ops_per_nonce_rounds"] - ops) < 0.01
     assert abs(rl["frac_rounds"] - ghs * ops / 78.6432e12) < 1e-3
+
+
+def test_roofline_prices_the_tiled_kernel_at_1552_per_compression(monkeypatch):
+    """cfg2's tiled kernel: frac = 1552 x C_eff (= C = 1) lane-ops per nonce,
+    equal to frac_algorithmic_C; frac_rounds beside it."""
+    monkeypatch.setattr(bench, "profiled", lambda k: (None, None, None, None))
+    st = {"dom_compressions": 1, "dom_compressions_eff": 1.0, "dom_launches": 2,
+          "dom_kernel_ms": 113.8, "dom_nonces": 4_194_967_296, "dom_grid": 1792,
+          "dom_kernel": "hm_tiled_kernel<4, false, false>"}
+    rl = bench.roofline(st, b"bradfitz", 0, 2**32 - 1)
+    ghs = 4_194_967_296 / 0.1138
+    assert rl["pricing"] == "1552 x C" and rl["ops_per_nonce"] == 1552
+    assert abs(rl["frac"] - ghs * 1552 / 78.6432e12) < 1e-3
+    assert rl["frac"] == rl["frac_algorithmic_C"]
+    assert rl["frac_rounds"] < rl["frac"]
+    assert rl["queue_units_per_launch"] == 4_194_967_296 // 2 // 6400
 
 
 def test_rounds_ops_of_the_tiled_kernel():
@@ -202,3 +221,39 @@ def test_wrong_answers_ignores_child_errors():
     assert len(bench.wrong_answers(line)) == 1
     line["ranks"]["match"] = [True, False]
     assert "primary" in bench.wrong_answers(line)
+
+
+def test_kfd_queue_sampler_reads_sysfs(tmp_path, monkeypatch):
+    """single_process.<merge>.queues_per_gpu: the queues (and processes) KFD
+    lists per GPU while a child runs, keyed by the GPU's PCI address from
+    KFD's topology; a host without KFD gives an error entry, not a failure."""
+    proc, topo = tmp_path / "proc", tmp_path / "nodes"
+    for pid, qs in {"101": ["1111", "1111", "2222"], "202": ["1111"], "303": []}.items():
+        for i, g in enumerate(qs):
+            d = proc / pid / "queues" / str(i)
+            d.mkdir(parents=True)
+            (d / "gpuid").write_text(g + "\n")
+        (proc / pid).mkdir(parents=True, exist_ok=True)
+    for n, (gid, loc) in enumerate([("0", None), ("1111", (0x75 << 8) | (0 << 3)),
+                                    ("2222", (0xf5 << 8) | (0 << 3))]):
+        d = topo / str(n)
+        d.mkdir(parents=True)
+        (d / "gpu_id").write_text(gid + "\n")
+        (d / "properties").write_text(("location_id %d\ndomain 0\n" % loc) if loc else "cpu 1\n")
+    monkeypatch.setattr(bench, "KFD_PROC", str(proc))
+    monkeypatch.setattr(bench, "KFD_TOPOLOGY", str(topo))
+    assert bench.kfd_queues() == {"1111": {"queues": 3, "processes": 2},
+                                  "2222": {"queues": 1, "processes": 1}}
+    assert bench.kfd_gpu_pci() == {"1111": "0000:75:00.0", "2222": "0000:f5:00.0"}
+    with bench.QueueSampler(period_s=0.01) as qs:
+        import time
+        time.sleep(0.05)
+    r = qs.result()
+    assert r["samples"] >= 1 and r["max_queues_any_gpu"] == 3
+    assert r["max"]["0000:75:00.0"] == {"queues": 3, "processes": 2}
+    monkeypatch.setattr(bench, "KFD_PROC", str(tmp_path / "none"))
+    with bench.QueueSampler(period_s=0.01) as qs:
+        pass
+    assert "error" in qs.result()
+    out = bench.run_single_process([0, 1], [0, 1], timeout=30, child_cmd=lambda m, d: ["true"])
+    assert "queues_per_gpu" in out["host"] and "queues_per_gpu" in out["rccl"]

@@ -121,3 +121,25 @@ def test_real_make_on_the_built_tree_reuses_everything():
     rep = entry.build_report(before, entry._artifacts(), None, 0.0)
     assert rep["mode"] == "reused", rep
     assert any(p.endswith("libhipminer.so") for p in rep["reused"])
+
+
+def test_smoke_prints_the_build_record(tmp_path):
+    """smoke() prints BUILD_REPORT's mode and compiled count next
+    to the build id, so the driver's GPU-test tail shows whether the box
+    compiled (stub reports; the real one is build()'s)."""
+    import json
+    rep = tmp_path / "BUILD_REPORT"
+    rep.write_text(json.dumps({"mode": "compiled", "compiled": ["a.o", "b.o", "lib.so"],
+                               "reused": ["x.hsaco"], "build_id": "0123456789abcdef",
+                               "seconds": 12.5}))
+    line = entry.build_record(str(rep))
+    assert line == ("build_report mode=compiled compiled=3 reused=1 "
+                    "build_id=0123456789abcdef seconds=12.5")
+    rep.write_text(json.dumps({"mode": "reused", "compiled": [], "reused": ["a.o"],
+                               "build_id": "f" * 16, "seconds": 0.4}))
+    assert entry.build_record(str(rep)).startswith("build_report mode=reused compiled=0 reused=1")
+    assert entry.build_record(str(tmp_path / "missing")).startswith("build_report none")
+    rep.write_text("{not json")
+    assert entry.build_record(str(rep)).startswith("build_report none")
+    src = open(entry.__file__).read()
+    assert "print(build_record()" in src.split("def smoke")[1]

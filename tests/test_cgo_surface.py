@@ -32,7 +32,7 @@ COMMAND = os.path.join(GOPATH, "src", "gpuminer", "main.go")
 
 CGO_BUILTINS = {"GoString", "GoStringN", "GoBytes", "CString", "CBytes", "malloc", "free",
                 "int", "uint", "char", "size_t", "uint8_t", "uint32_t", "uint64_t", "int64_t"}
-GO_STD = {"encoding/json", "fmt", "os", "strconv", "strings", "unsafe", "errors", "sync"}
+GO_STD = {"encoding/json", "fmt", "os", "strconv", "strings", "unsafe", "errors", "sync", "time"}
 
 
 def _read(p):
@@ -118,7 +118,7 @@ def test_every_c_name_is_declared_and_calls_match_arity():
     names = set(re.findall(r"\bC\.(\w+)", src))
     assert {"hm_open", "hm_scan", "hm_scan_many", "hm_scan_checked", "hm_partition",
             "hm_hash", "hm_close", "hm_strerror", "hm_scan_cpu", "HM_ERR_INVALID",
-            "HM_ERR_NO_DEVICE"} <= names
+            "HM_ERR_NO_DEVICE", "HM_ERR_TIMEOUT", "HM_OPT_DEADLINE_MS", "hm_set_option"} <= names
     for n in sorted(names - CGO_BUILTINS):
         declared = n in protos or re.search(rf"(\btypedef struct {n}\b|}} {n};|^#define {n}\b)", hdr, re.M)
         assert declared, f"C.{n} is not declared by include/hipminer.h"
@@ -222,3 +222,108 @@ def test_preamble_and_call_replay_compile_link_and_run(tmp_path, golden):
     import torch
     if not torch.cuda.is_available():
         assert int(rc0) == int(rc1) == _lib.HM_ERR_NO_DEVICE and why
+
+
+SERVE_REPLAY = r"""
+#include <stdio.h>
+#include <string.h>
+#include <time.h>
+
+/* gpuminer's serve() (go/src/gpuminer/main.go) per Request, in C with the
+   binding's calls: reopen the GPU after the backoff (Open + SetDeadline), the
+   GPU scan through EvalRequest's Upper+1 wrap, and on any failure -- no
+   context, a failed scan, ErrTimeout -- Close, back off and answer from
+   EvalRequestCPU (hm_scan_cpu).  Input lines: "<msg_hex> <lower> <upper>";
+   output: "<hash> <nonce> <gpu|host>". */
+typedef struct { hm_ctx *m; double retry_at, backoff; int opens; } gpu;
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+static void back_off(gpu *g) {
+    g->retry_at = now_s() + g->backoff;
+    g->backoff = g->backoff * 2 < 1 ? 1 : (g->backoff * 2 > 60 ? 60 : g->backoff * 2);
+}
+static int gpu_open(gpu *g) {
+    hm_ctx *c = NULL;
+    int ds[1] = {0};
+    ++g->opens;
+    int rc = hm_open(&ds[0], (int)1, &c);                                  /* Open(0) */
+    if (rc == HM_OK) rc = hm_set_option(c, HM_OPT_DEADLINE_MS, (int64_t)-1); /* SetDeadline(Auto) */
+    if (rc != HM_OK) { if (c) hm_close(c); return rc; }
+    g->m = c;
+    return HM_OK;
+}
+/* EvalRequest / EvalRequestCPU: the miner.go:52 wrap, then the inclusive scan */
+static int eval(hm_ctx *m, const uint8_t *p, size_t len, uint64_t lower, uint64_t upper,
+                uint64_t *h, uint64_t *n) {
+    uint64_t end = upper + 1;
+    if (!(lower < end)) { *h = ~0ull; *n = 0; return HM_OK; }
+    hm_result out;
+    int rc = m ? hm_scan(m, p, len, lower, end - 1, &out)
+               : hm_scan_cpu(p, len, lower, end - 1, (int)0, &out);
+    if (rc == HM_OK) { *h = out.hash; *n = out.nonce; }
+    return rc;
+}
+
+int main(void) {
+    gpu g = {NULL, 0, 0, 0};
+    if (gpu_open(&g) != HM_OK) back_off(&g);                                 /* main() */
+    char hex[4096];
+    unsigned long long lower, upper;
+    while (scanf("%4095s %llu %llu", hex, &lower, &upper) == 3) {
+        size_t len = strcmp(hex, "-") ? strlen(hex) / 2 : 0;
+        uint8_t buf[2048];
+        for (size_t i = 0; i < len; ++i) sscanf(hex + 2 * i, "%2hhx", &buf[i]);
+        if (!g.m && now_s() >= g.retry_at && gpu_open(&g) != HM_OK) back_off(&g);
+        uint64_t h = 0, n = 0;
+        int rc = HM_ERR_NO_DEVICE;
+        const char *where = "host";
+        if (g.m) {
+            rc = eval(g.m, len ? buf : NULL, len, lower, upper, &h, &n);
+            if (rc == HM_OK) where = "gpu";
+            else { hm_close(g.m); g.m = NULL; back_off(&g); }
+        }
+        if (rc != HM_OK && eval(NULL, len ? buf : NULL, len, lower, upper, &h, &n) != HM_OK)
+            return 2;
+        printf("%llu %llu %s\n", (unsigned long long)h, (unsigned long long)n, where);
+    }
+    if (g.m) hm_close(g.m);
+    fprintf(stderr, "opens %d\n", g.opens);
+    return 0;
+}
+"""
+
+
+def test_serve_fallback_replay_without_gpu(tmp_path, golden):
+    """the Go gpuminer's fallback sequence is not compiled here, so
+    its C replay is: with no visible GPU every Open fails, the Requests --
+    the golden miner-eval KATs, the Upper = 2^64-1 wrap included -- are
+    answered by hm_scan_cpu with the oracle's Results, and Open is retried
+    only after the backoff (1 s, then doubling), not per Request."""
+    pre = _preamble(_read(BINDING))
+    srcdir = os.path.dirname(BINDING)
+    flags = {k: v.replace("${SRCDIR}", srcdir).split()
+             for k, v in re.findall(r"#cgo (CFLAGS|LDFLAGS):(.*)", pre)}
+    includes = "\n".join(l for l in pre.splitlines() if l.startswith("#include"))
+    src = tmp_path / "serve.c"
+    src.write_text(includes + "\n" + SERVE_REPLAY)
+    exe = tmp_path / "serve"
+    subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+                    *flags["CFLAGS"], "-o", str(exe), str(src), *flags["LDFLAGS"]], check=True)
+    kats = golden["miner_eval_kats"]
+    feed = "".join(f"{k['msg_hex'] or '-'} {k['lower']} {k['upper']}\n" for k in kats)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1")
+    r = subprocess.run([str(exe)], input=feed, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    got = [l.split() for l in r.stdout.strip().splitlines()]
+    assert len(got) == len(kats)
+    for k, (h, n, where) in zip(kats, got):
+        assert (int(h), int(n)) == (int(k["hash"]), int(k["nonce"])), k
+        assert where == "host"
+    # the first Open at start; the backoff (>= 1 s) keeps the quick Requests
+    # from re-trying it each time
+    assert "opens 1" in r.stderr or "opens 2" in r.stderr, r.stderr

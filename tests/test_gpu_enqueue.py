@@ -2,9 +2,9 @@
 
 Chained f >= 5 segments grow their stream's K+W table (10^5 .. 10^7 rows).
 Work queued earlier may still read the old table, so it is retired (api.cpp
-kw_table_rows; freed at the end of the call since ABI 1.7, after the host
-has waited for the call's work) instead of freed, which would drain the
-device mid-enqueue: every device of a
+kw_table_rows; freed at hm_close -- ABI 1.7 freed it at the end of the call,
+but hipFree waits for the whole device, other contexts' work included)
+instead of freed, which would drain the device mid-enqueue: every device of a
 context gets its work before the host waits on any of it (one
 context drives all of a miner's GPUs).  hm_stats counts the waits issued while
 enqueuing (mid_call_syncs), the tables grown (table_grows) and the host time
@@ -122,3 +122,32 @@ def test_mid_call_sync_counter_counts(oracle_mod):
         c.set_option(_lib.HM_OPT_TEST_MID_SYNC, 0)
         assert c.scan(m, lo, hi) == exp
         assert c.stats()["mid_call_syncs"] == 0
+
+
+def test_streams_are_made_on_first_use(oracle_mod):
+    """ABI 1.8 (hardware-queue headroom of the N = 8 line): hm_open
+    makes stream 0 only; fused requests stay on it; a multi-segment request
+    makes the tail streams up to HM_OPT_STREAMS and no more; answers equal
+    the fixture throughout."""
+    from distributed_bitcoinminer_amd import _lib
+    with _lib.Context([0]) as c:
+        assert c.streams_made() == 1
+        assert c.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)  # fused
+        assert c.scan_many([(b"x", 0, 999), (b"y", 5, 50_000)]) == \
+            [oracle_mod.c_scan(b"x", 0, 999), oracle_mod.c_scan(b"y", 5, 50_000)]
+        assert c.streams_made() == 2  # two fused requests of a batch: two streams
+        c.set_option(_lib.HM_OPT_STREAMS, 2)
+        # one digit segment, far above the fused size: stream 0 alone
+        lo = 10**11
+        assert c.scan(b"bradfitz", lo, lo + 10**9) == oracle_mod.fast_scan_sum(
+            b"bradfitz", lo, lo + 10**9)[0]
+        assert c.streams_made() == 2
+        assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+        assert c.streams_made() == 2
+        c.set_option(_lib.HM_OPT_STREAMS, 4)
+        assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+        assert c.streams_made() == 4
+    with _lib.Context([0]) as c:
+        c.set_option(_lib.HM_OPT_STREAMS, 1)
+        assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+        assert c.streams_made() == 1

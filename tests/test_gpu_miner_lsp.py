@@ -215,8 +215,9 @@ def test_server_sim_reassigns_a_killed_miner(oracle_mod):
 def test_miner_falls_back_to_host_after_a_failed_gpu_scan(oracle_mod):
     """SURVEY §8(b) liveness, mid-run: the GPU answers the first Request, the
     second GPU scan fails (HM_MINER_TEST_FAIL_AFTER=1 injects HM_ERR_HIP), and
-    that Request and every later one are still answered, on the host
-    (hm_scan_cpu), with the oracle's Results; the miner says so on stderr."""
+    that Request is answered on the host (hm_scan_cpu) and every later one
+    too (on the host until the 1-s retry backoff passes, then on a reopened
+    GPU context), with the oracle's Results; the miner says so on stderr."""
     srv = H.FakeLspServer(epoch_ms=100, epoch_limit=50)
     env = dict(ENV, HM_MINER_TEST_FAIL_AFTER="1", HM_CPU_THREADS="8")
     p = subprocess.Popen([MINER, srv.hostport], env=env, stdout=subprocess.PIPE,

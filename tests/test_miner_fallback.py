@@ -53,3 +53,44 @@ def test_miner_without_gpu_answers_on_the_host(oracle_mod, golden):
     err = p.stderr.read()
     assert p.returncode == 0, err
     assert "NO GPU" in err and "hm_scan_cpu" in err, err
+
+
+def _run_miner(env_extra, timeout=60):
+    env = dict(os.environ, HM_LSP_EPOCH_MS="100", HM_LSP_EPOCH_LIMIT="20",
+               HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1", HM_CPU_THREADS="2",
+               **env_extra)
+    srv = H.FakeLspServer(epoch_ms=100, epoch_limit=20)
+    p = subprocess.Popen([MINER, srv.hostport], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    got = None
+    try:
+        if p.poll() is None:
+            try:
+                cid = srv.accept(timeout=10)
+                assert srv.read(cid, timeout=60) == bitcoin.marshal(bitcoin.NewJoin())
+                got = _ask(srv, cid, "bradfitz", 0, 9999)
+            except Exception:  # the miner exited before joining
+                pass
+    finally:
+        srv.close()
+        try:
+            p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return p.returncode, got, p.stderr.read()
+
+
+def test_miner_device_list_parse_errors_are_fatal_the_rest_falls_back():
+    """only a malformed HIPMINER_DEVICES ends hm_miner (exit 1,
+    before it joins); a well-formed list naming a GPU that is not there --
+    here none is visible -- falls back to the host scan like no GPU at all."""
+    assert os.path.exists(MINER), "build hm_miner first (__graft_entry__.build())"
+    for bad in ("x", "0,a", "-1", "1.5"):
+        rc, got, err = _run_miner({"HIPMINER_DEVICES": bad})
+        assert rc == 1 and got is None, (bad, rc, err)
+        assert "bad HIPMINER_DEVICES" in err, err
+    for ok in ("7", " 0 , 3 ", "63,"):
+        rc, got, err = _run_miner({"HIPMINER_DEVICES": ok})
+        assert rc == 0 and got == (1419516646206828, 9898), (ok, rc, err)
+        assert "NO GPU" in err, err

@@ -2,7 +2,9 @@
 of what one rank of the N-GPU bench line does on its GPU, from KFD's
 per-process sysfs (/sys/class/kfd/kfd/proc/<pid>/queues/<qid>/{gpuid,type}):
 torch's CUDA context, a torch stream, an RCCL (world-1) all-gather, a hipminer
-context with its 4 streams, the scan, and after hm_close.  DESIGN §6 uses the
+context (streams made on first use since ABI 1.8; HM_QC_STREAMS = its
+HM_OPT_STREAMS, default 2 as in bench.py), a fused and a multi-segment scan,
+and after hm_close.  DESIGN §6 uses the
 counts to price the processes and hardware queues per GPU of the N = 8 line.
 One JSON line per stage."""
 import json
@@ -78,10 +80,14 @@ def main():
     torch.cuda.synchronize()
     stage("RCCL world-1 all-gather")
     from distributed_bitcoinminer_amd import _lib
+    streams = int(os.environ.get("HM_QC_STREAMS", "2"))
     c = _lib.Context([0])
-    stage("hm_open (4 streams)")
-    c.scan(b"bradfitz", 0, 10**8)
-    stage("hm_scan [0, 10^8]")
+    c.set_option(_lib.HM_OPT_STREAMS, streams)
+    stage("hm_open (ABI 1.8: stream 0 only)")
+    c.scan(b"bradfitz", 0, 10**7)
+    stage("hm_scan [0, 10^7] (fused launch, stream 0)")
+    c.scan(b"bradfitz", 0, 2**32 - 1)
+    stage(f"hm_scan [0, 2^32) with HM_OPT_STREAMS={streams}")
     c.close()
     stage("hm_close")
     dist.destroy_process_group()
