@@ -177,7 +177,7 @@ def test_scan_stats_writes_only_the_frozen_144_bytes(ctx):
     buf = (ctypes.c_uint8 * 256)(*([0xA5] * 256))
     assert lib.hm_scan_stats(ctx._h, ctypes.cast(buf, ctypes.POINTER(_lib.hm_stats))) == 0
     assert all(b == 0xA5 for b in buf[144:]), "hm_scan_stats wrote past 144 bytes"
-    st = _lib.hm_stats.from_buffer_copy(bytes(buf[:160]))
+    st = _lib.hm_stats.from_buffer_copy(bytes(buf[:ctypes.sizeof(_lib.hm_stats)]))
     full = ctx.stats()
     assert st.nonces == full["nonces"] == 100_000
     assert st.dom_compressions_eff == full["dom_compressions_eff"] > 0
