@@ -8,7 +8,12 @@ set -o pipefail
 export TMPDIR=/tmp
 O=${1:-gpurun_out/r06a}
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+prc=$?
+tail -3 $O/pytest_gpu.log
+# test failures (rc 1) still let the measurements run; a time limit, abort
+# or crash ends the call here
+if [ $prc -gt 1 ]; then echo "pytest rc=$prc: stopping"; exit $prc; fi
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
 timeout -k 10 120 python -u tools/queue_count.py > $O/queue_count.jsonl 2> $O/queue_count.err &&
 timeout -k 10 200 python -u tools/ab_opts.py 15 s4:STREAMS=4 s2:STREAMS=2 > $O/ab_streams_cfg2.jsonl 2> $O/ab.err &&
