@@ -34,6 +34,9 @@ HM_OPT_FUSED = 10
 HM_OPT_FUSED_FLAGS = 11
 HM_OPT_FUSED_PARTS = 12
 HM_OPT_DEADLINE_MS = 13
+HM_OPT_FUSED_TAIL = 14
+HM_OPT_TAIL_FUSED = 15
+HM_OPT_HOST_RESULT = 16
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 

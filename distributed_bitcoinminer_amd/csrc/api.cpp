@@ -57,6 +57,9 @@ constexpr uint64_t kConcurrentNonces = 1ull << 27;
 constexpr int kFusedPerCu = 3;
 constexpr uint32_t kFusedDefaultFlags = kFusedStaticFirst;
 constexpr uint32_t kFusedDefaultParts = 1;  // tiled fused tasks: one tens digit (10 steps)
+// Guided tail of a fused launch (HM_OPT_FUSED_TAIL): the last ~one wave-round
+// of tasks is cut into this many pieces each.
+constexpr uint32_t kFusedDefaultTail = 5;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -111,7 +114,8 @@ struct Device {
     uint64_t* best = nullptr;      // [kMaxBatch][kStreams][2]: per request, per stream
     uint64_t* result = nullptr;    // [kMaxBatch][2]
     uint64_t* gathered = nullptr;  // [ndev][kMaxBatch][2] (RCCL merge)
-    hm_result* host_out = nullptr; // pinned [kMaxBatch]
+    hm_result* host_out = nullptr; // pinned, fine-grained [kMaxBatch]: the 16-B readback slots
+    uint64_t* host_dev = nullptr;  // host_out as the device addresses it
     hipEvent_t join[kStreams] = {};
     hipEvent_t gate = nullptr;     // stream 0 reached its last dominant segment
     hipEvent_t t0 = nullptr;       // timing origin of the current call
@@ -155,6 +159,9 @@ struct hm_ctx {
     bool fused = true;            // HM_OPT_FUSED: small requests in one launch
     uint32_t fused_flags = kFusedDefaultFlags;  // HM_OPT_FUSED_FLAGS (experiment hook)
     uint32_t fused_parts = kFusedDefaultParts;  // HM_OPT_FUSED_PARTS (experiment hook)
+    uint32_t fused_tail = kFusedDefaultTail;    // HM_OPT_FUSED_TAIL (1 = no split)
+    bool tail_fused = true;  // HM_OPT_TAIL_FUSED: a large request's tail segments in one fused launch
+    bool host_result = true; // HM_OPT_HOST_RESULT: results stored to pinned host memory by the last fold
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -226,7 +233,11 @@ int device_init(Device& dv, int ordinal) {
     HIPCHK(hipMalloc(&dv.best, (size_t)kMaxBatch * kStreams * 2 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&dv.acc, (size_t)kStreams * 2 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&dv.result, (size_t)kMaxBatch * 2 * sizeof(uint64_t)));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), kMaxBatch * sizeof(hm_result)));
+    // fine-grained (coherent) pinned memory: the last fold kernel of a call
+    // stores the results here with system-scope stores (HM_OPT_HOST_RESULT)
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&dv.host_out), kMaxBatch * sizeof(hm_result),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&dv.host_dev), dv.host_out, 0));
     return HM_OK;
 }
 
@@ -724,7 +735,7 @@ int fused_rank(const SegPlan& g) {
 // -> hm_fold_kernel into *best.  Tasks are ordered costliest layout first,
 // larger segments first.
 int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPlan> segs, int si,
-                  uint64_t* best, bool seed_best) {
+                  uint64_t* best, bool seed_best, uint64_t* host = nullptr) {
     hipStream_t st = dv.stream[si];
     std::stable_sort(segs.begin(), segs.end(), [](const SegPlan& a, const SegPlan& b) {
         if (fused_rank(a) != fused_rank(b)) return fused_rank(a) < fused_rank(b);
@@ -756,7 +767,8 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     memcpy(fa.mid, mp.mid, sizeof fa.mid);
     uint64_t tasks = 0, jobs = 0, nonces = 0;
     uint32_t rec_next = 0, aux_next = 0, comp_max = 1;
-    double comp_w = 0;  // executed compressions x nonces (hm_stats)
+    std::vector<double> ce_base(segs.size()), seg_units(segs.size());  // chained C_eff inputs
+    std::vector<uint64_t> seg_cnt(segs.size());
     for (size_t i = 0; i < segs.size(); ++i) {
         const SegPlan& g = segs[i];
         FusedSeg& S = fa.segs[i];
@@ -803,7 +815,10 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
                 seg_tasks = nunits * S.tpu;
                 seg_jobs = nt + pow10_u64(g.f);
                 aux_next += (uint32_t)pow10_u64(g.f) * 64;
-                ce = 1.0 + (double)seg_tasks / ((double)nunits * (double)g.tch);
+                // 1 + block-0 compressions per loop value: one per task (and
+                // per guided-tail piece, added below)
+                ce = 1.0;
+                seg_units[i] = (double)nunits * (double)g.tch;
             } else {
                 S.variant = P.variant = (uint32_t)(g.W1 * 4 + (g.straddle ? 2 : 0) + (g.trailer ? 1 : 0));
                 S.lane_shift = g.lane_shift;
@@ -825,11 +840,33 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
         P.job_end = (uint32_t)jobs;
         nonces += cnt;
         comp_max = std::max(comp_max, g.nb);
-        comp_w += ce * (double)cnt;
+        ce_base[i] = ce;
+        seg_cnt[i] = cnt;
     }
-    if (tasks >= (1ull << 31) || jobs >= (1ull << 31) || aux_next > kFusedAuxWords)
+    // guided tail: the last min(tasks, one wave-round of the occupancy grid)
+    // tasks -- the cheapest layouts, queued last -- run as fused_tail pieces
+    // each (the grid is then sized by ids, pieces included)
+    const uint64_t cap_waves =
+        (uint64_t)persistent_grid(ctx, dv, kFusedPerCu, 1ull << 40) * (kBlock / kWaveSize);
+    const uint32_t nparts = ctx->fused_tail;
+    const uint64_t nsplit = nparts > 1 ? std::min<uint64_t>(tasks, cap_waves) : 0;
+    const uint64_t nbig = tasks - nsplit;
+    const uint64_t ids = nbig + nsplit * nparts;
+    if (ids >= (1ull << 31) || jobs >= (1ull << 31) || aux_next > kFusedAuxWords)
         return HM_ERR_INTERNAL;  // excluded by fusible()
-    fa.ntasks = (uint32_t)tasks;
+    double comp_w = 0;  // executed compressions x nonces (hm_stats)
+    for (size_t i = 0; i < segs.size(); ++i) {
+        double ce = ce_base[i];
+        if (seg_units[i] > 0) {  // chained: block 0 per task, and per piece of a split task
+            const uint64_t a = i ? fa.segs[i - 1].task_end : 0, b = fa.segs[i].task_end;
+            const uint64_t split = b > std::max(a, nbig) ? b - std::max(a, nbig) : 0;
+            ce += (double)(b - a + split * (nparts - 1)) / seg_units[i];
+        }
+        comp_w += ce * (double)seg_cnt[i];
+    }
+    fa.ntasks = (uint32_t)ids;
+    fa.nbig = (uint32_t)nbig;
+    fa.nparts = nparts > 1 ? nparts : 1;
     fa.nseg = pa.nseg = (uint32_t)segs.size();
     pa.njobs = (uint32_t)jobs;
     const Device::Fn* fn = nullptr;
@@ -837,7 +874,7 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     if (rc) return rc;
     // small launches: few waves per SIMD keep a task short, so the launch's
     // tail is short (kFusedPerCu = 3 workgroups per CU, profiles/r05/fused/)
-    const int grid = persistent_grid(ctx, dv, kFusedPerCu, tasks);
+    const int grid = persistent_grid(ctx, dv, kFusedPerCu, ids);
     fa.flags = ctx->fused_flags;
     // with static first tasks the queue starts past every wave slot
     pa.counter0 = (fa.flags & kFusedStaticFirst) ? (uint32_t)grid * (kBlock / kWaveSize) : 0;
@@ -857,7 +894,7 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     rc = launch_scan(*fn, fa, grid, st);
     if (rc) return rc;
     HIPCHK(hipEventRecord(L.stop, st));
-    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best, st));
+    HIPCHK(launch_fold(dv.cand[si], (uint32_t)grid * (kBlock / kWaveSize), best, st, 1, host));
     if (ctx->csum)
         HIPCHK(launch_sum_fold(dv.sums[si], (uint32_t)grid * (kBlock / kWaveSize), dv.acc + 2 * si,
                                st));
@@ -872,10 +909,13 @@ struct DevReq {
 };
 
 // Enqueue a batch of scans on one device; request r's result lands in
-// dv.result + 2r.  All segments of all requests are queued before any sync.
-// `first`: the call's first chunk, which records the timing origin dv.t0
-// (every launch of an hm_scan_many call is timed against it).
-int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& reqs, bool first) {
+// dv.result + 2r, and with `to_host` also in the pinned readback slot
+// dv.host_out[r] (stored by the last fold kernel).  All segments of all
+// requests are queued before any sync.  `first`: the call's first chunk,
+// which records the timing origin dv.t0 (every launch of an hm_scan_many
+// call is timed against it).
+int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& reqs, bool first,
+                         bool to_host) {
     HIPCHK(hipSetDevice(dv.ordinal));
     const int n = (int)reqs.size();
     hipStream_t s0 = dv.stream[0];
@@ -886,7 +926,9 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
     if (n == 1 && !reqs[0].empty && ctx->fused && !ctx->test_mid_sync) {
         std::vector<SegPlan> segs = plan_range(*reqs[0].mp, reqs[0].lo, reqs[0].hi,
                                                ctx->force_generic, ctx->table_digits);
-        if (fusible(segs)) return enqueue_fused(ctx, dv, *reqs[0].mp, segs, 0, dv.result, true);
+        if (fusible(segs))
+            return enqueue_fused(ctx, dv, *reqs[0].mp, segs, 0, dv.result, true,
+                                 to_host ? dv.host_dev : nullptr);
     }
     // streams == 1: every segment in order on stream 0, so kernels never
     // overlap and per-kernel timings match rocprofv3 exactly.  streams > 1:
@@ -906,7 +948,9 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
         std::vector<SegPlan> segs;
         int dom = -1;            // the key with the most nonces
         long double total = 0;   // nonces
-        bool fused = false;
+        bool fused = false;      // the whole request in one fused launch
+        std::vector<SegPlan> tail;  // segments off the dominant key (large requests)
+        bool tail_fused = false;    // ... run as one fused launch
     };
     // plan every request first: the streams the batch needs are made (once
     // per context, make_streams) before anything is queued on them
@@ -936,8 +980,13 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
         } else if (P.total <= (long double)kConcurrentNonces) {
             used = std::max(used, std::min(nstreams, (int)P.segs.size()));
         } else {
-            int off = 0;  // segments off the dominant key: the tail streams
-            for (const auto& g : P.segs) off += key(g) != P.dom;
+            // segments off the dominant key run in its tail: as ONE fused
+            // launch when they fit it (cfg2's d <= 8, cfg3's trailer
+            // segments), else one launch each on the tail streams
+            for (const auto& g : P.segs)
+                if (key(g) != P.dom) P.tail.push_back(g);
+            P.tail_fused = ctx->fused && ctx->tail_fused && fusible(P.tail);
+            const int off = P.tail_fused ? 1 : (int)P.tail.size();
             used = std::max(used, std::min(nstreams, 1 + off));
         }
     }
@@ -992,6 +1041,14 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
             if (pass == 1)
                 for (int q = 1; q < ns; ++q)
                     HIPCHK(hipStreamWaitEvent(dv.stream[q], dv.gate, 0));
+            if (pass == 1 && plans[r].tail_fused) {
+                // every tail segment in one fused launch on a tail stream
+                const int si = 1 + (rr++ % (ns - 1));
+                int rc = enqueue_fused(ctx, dv, *reqs[r].mp, plans[r].tail, si, best + 2 * si,
+                                       false);
+                if (rc) return rc;
+                continue;
+            }
             for (size_t i = 0; i < segs.size(); ++i) {
                 int si = 0;
                 if (ns > 1) {
@@ -1010,7 +1067,8 @@ int enqueue_device_batch(hm_ctx* ctx, Device& dv, const std::vector<DevReq>& req
         HIPCHK(hipStreamWaitEvent(s0, dv.join[s], 0));
     }
     for (int r = 0; r < n; ++r)
-        HIPCHK(launch_fold(dv.best + (size_t)r * kStreams * 2, kStreams, dv.result + 2 * r, s0));
+        HIPCHK(launch_fold(dv.best + (size_t)r * kStreams * 2, kStreams, dv.result + 2 * r, s0, 1,
+                           to_host ? dv.host_dev + 2 * r : nullptr));
     return HM_OK;
 }
 
@@ -1059,7 +1117,7 @@ int rccl_merge(hm_ctx* ctx, int nreq) {
     HIPCHK(launch_init_best(d0.result, (uint32_t)nreq, d0.stream[0]));
     for (int r = 0; r < nreq; ++r)
         HIPCHK(launch_fold(d0.gathered + 2 * r, (uint32_t)n, d0.result + 2 * r, d0.stream[0],
-                           (uint32_t)nreq));
+                           (uint32_t)nreq, ctx->host_result ? d0.host_dev + 2 * r : nullptr));
     return HM_OK;
 }
 
@@ -1090,7 +1148,8 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
     const auto te = std::chrono::steady_clock::now();
     ctx->enqueuing = true;
     for (int i = 0; i < ndev; ++i) {
-        int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i], first);
+        int rc = enqueue_device_batch(ctx, ctx->devs[i], per_dev[i], first,
+                                      ctx->host_result && !ctx->merge_rccl);
         if (rc) { ctx->enqueuing = false; return rc; }
     }
     ctx->enqueuing = false;
@@ -1102,8 +1161,9 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
         ctx->merge = HM_MERGE_RCCL;
         Device& d0 = ctx->devs[0];
         HIPCHK(hipSetDevice(d0.ordinal));
-        HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, nreq * sizeof(hm_result),
-                              hipMemcpyDeviceToHost, d0.stream[0]));
+        if (!ctx->host_result)
+            HIPCHK(hipMemcpyAsync(d0.host_out, d0.result, nreq * sizeof(hm_result),
+                                  hipMemcpyDeviceToHost, d0.stream[0]));
         for (auto& dv : ctx->devs) {
             HIPCHK(hipSetDevice(dv.ordinal));
             int rc = host_wait(ctx, dv.stream[0]);
@@ -1114,6 +1174,7 @@ int scan_chunk(hm_ctx* ctx, const hm_request* reqs, int nreq, hm_result* outs, b
     }
     ctx->merge = ndev > 1 ? HM_MERGE_HOST : HM_MERGE_NONE;
     for (auto& dv : ctx->devs) {
+        if (ctx->host_result) break;  // the last fold stored them in host_out
         HIPCHK(hipSetDevice(dv.ordinal));
         HIPCHK(hipMemcpyAsync(dv.host_out, dv.result, nreq * sizeof(hm_result),
                               hipMemcpyDeviceToHost, dv.stream[0]));
@@ -1284,6 +1345,16 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
         case HM_OPT_FUSED_PARTS:
             if (value != 1 && value != 2 && value != 5 && value != 10) return HM_ERR_INVALID;
             ctx->fused_parts = (uint32_t)value;
+            return HM_OK;
+        case HM_OPT_HOST_RESULT:
+            ctx->host_result = value != 0;
+            return HM_OK;
+        case HM_OPT_TAIL_FUSED:
+            ctx->tail_fused = value != 0;
+            return HM_OK;
+        case HM_OPT_FUSED_TAIL:
+            if (value != 1 && value != 2 && value != 5 && value != 10) return HM_ERR_INVALID;
+            ctx->fused_tail = (uint32_t)value;
             return HM_OK;
         case HM_OPT_GRID_PER_CU:
             if (value < 0 || value > 32) return HM_ERR_INVALID;

@@ -16,6 +16,8 @@
 //   chained (f <= 4 final-block digits, one K+W table): 64 lanes x up to
 //          100 table-driven blocks, block 0 per lane per task;
 //   generic: 64 lanes x 10 nonces, the byte-level tail builder.
+// The last ~one wave-round of tasks is split into FusedArgs::nparts pieces
+// (a guided tail), so the launch ends on pieces of a task, not whole tasks.
 // The wave keeps one running (hash, nonce) minimum across all its tasks
 // (one request), written to its candidate slot at exit; hm_fold_kernel then
 // reduces the slots.  Tables (tile records, sigma0 of the loop digits, the
@@ -36,29 +38,42 @@ namespace hm {
 // runtime segment index, a by-value parameter would be copied to scratch.
 typedef const __attribute__((address_space(4))) FusedArgs FusedArgsK;
 
+// Piece `pp` of `np` of the run [b, e): [*b2, *e2) (empty when past e).
+DEV void piece_of(uint32_t b, uint32_t e, uint32_t pp, uint32_t np, uint32_t* b2, uint32_t* e2) {
+    const uint32_t len = (e - b + np - 1) / np;
+    uint32_t x = b + pp * len, y = x + len;
+    if (x > e) x = e;
+    if (y > e) y = e;
+    *b2 = x;
+    *e2 = y;
+}
+
 template <int W1, bool STRADDLE, bool TRAILER, bool CSUM>
-DEV void fused_tiled(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& best,
-                     WaveSums& sums) {
+DEV void fused_tiled(FusedArgsK* A, const FusedSeg& S, uint32_t k, uint32_t pp, uint32_t np,
+                     WaveBest& best, WaveSums& sums) {
     // task k: unit, tens digit t1 and part of the units loop (S.tpu parts
-    // of 10 / S.tpu steps each)
+    // of 10 / S.tpu steps each); a guided-tail piece pp of np runs a share
+    // of that part's steps
     const uint32_t per_unit = 10u * S.tpu;
     const uint32_t unit = S.unit0 + k / per_unit;
     const uint32_t rem = k - (k / per_unit) * per_unit;
     const uint32_t t1 = rem / S.tpu;
     const uint32_t part = rem - t1 * S.tpu;
     const uint32_t steps = 10u / S.tpu;
+    uint32_t t0b, t0e;
+    piece_of(part * steps, part * steps + steps, pp, np, &t0b, &t0e);
     const uint32_t tile = unit / S.tpt;
     const uint32_t chunk = unit - tile * S.tpt;
     const_u32* tab = (const_u32*)(A->aux + S.aux0);
     tiled_task<W1, STRADDLE, TRAILER, CSUM>(A->rec + (size_t)(S.rec0 + tile) * kRecWords, chunk, t1,
                                             t1 + 1, (S.tile0 + tile) * S.pow10V, S.seg_lo, S.seg_hi,
                                             S.vmax, S.q, S.lane_shift, S.loop_shift, tab, tab + 100,
-                                            best, sums, part * steps, part * steps + steps);
+                                            best, sums, t0b, t0e);
 }
 
 template <bool CSUM>
-DEV void fused_chained(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& best,
-                       WaveSums& sums) {
+DEV void fused_chained(FusedArgsK* A, const FusedSeg& S, uint32_t k, uint32_t pp, uint32_t np,
+                       WaveBest& best, WaveSums& sums) {
     const uint32_t unit = S.unit0 + k / S.tpu;
     const uint32_t part = k - (k / S.tpu) * S.tpu;
     const uint32_t per_tile = S.tpt * S.ntc;
@@ -70,16 +85,20 @@ DEV void fused_chained(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& b
     const uint32_t t_begin = tc * S.tch + part * piece;
     uint32_t t_end = tc * S.tch + S.tch;
     if (t_end > t_begin + piece) t_end = t_begin + piece;
-    chained_task<CSUM>(A->rec + (size_t)(S.rec0 + tile) * kRecWords, chunk, t_begin, t_end,
+    uint32_t tb, te;
+    piece_of(t_begin, t_end, pp, np, &tb, &te);
+    if (tb >= te) return;  // uniform
+    chained_task<CSUM>(A->rec + (size_t)(S.rec0 + tile) * kRecWords, chunk, tb, te,
                        (S.tile0 + tile) * S.pow10V, S.pow10f, S.seg_lo, S.seg_hi, S.vmax, S.q,
                        A->aux + S.aux0, best, sums);
 }
 
-// Generic task k: nonces seg_lo + 640k + lane + 64j, j < 10, one per lane
-// and step, every tail block compressed per lane.
+// Generic task k: nonces seg_lo + 640k + lane + 64j, j < 10 (a guided-tail
+// piece: its share of the j), one per lane and step, every tail block
+// compressed per lane.
 template <bool CSUM>
-DEV void fused_generic(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& best,
-                       WaveSums& sums) {
+DEV void fused_generic(FusedArgsK* A, const FusedSeg& S, uint32_t k, uint32_t pp, uint32_t np,
+                       WaveBest& best, WaveSums& sums) {
     const uint32_t lane = __lane_id();
     uint32_t pw[16], mid[8];
 #pragma unroll
@@ -87,7 +106,9 @@ DEV void fused_generic(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& b
 #pragma unroll
     for (int i = 0; i < 8; ++i) mid[i] = A->mid[i];
     const uint64_t base = S.seg_lo + (uint64_t)k * 640u;
-    for (uint32_t j = 0; j < 10; ++j) {
+    uint32_t jb, je;
+    piece_of(0, 10, pp, np, &jb, &je);
+    for (uint32_t j = jb; j < je; ++j) {
         const uint64_t nb0 = base + 64u * j;  // wave-uniform
         if (nb0 > S.seg_hi || nb0 < S.seg_lo) break;  // past the end (or wrapped)
         const uint64_t n = nb0 + lane;
@@ -117,7 +138,7 @@ DEV void fused_generic(FusedArgsK* A, const FusedSeg& S, uint32_t k, WaveBest& b
 }
 
 #define HM_FUSED_CASE(W, S, T) \
-    case (W) * 4 + (S) * 2 + (T): fused_tiled<W, S, T, CSUM>(A, S_, k, best, sums); break;
+    case (W) * 4 + (S) * 2 + (T): fused_tiled<W, S, T, CSUM>(A, S_, k, pp, np, best, sums); break;
 #define HM_FUSED_CASE_S(W, T) HM_FUSED_CASE(W, false, T) HM_FUSED_CASE(W, true, T)
 
 template <bool CSUM>
@@ -143,12 +164,21 @@ DEV void fused_body(FusedArgsK* A) {
         return t;
     };
     uint32_t next = (flags & (kFusedStaticFirst | kFusedStatic)) ? wslot : dequeue();
+    const uint32_t nbig = A->nbig, nparts = A->nparts;
     for (;;) {
-        const uint32_t task = uni(next);
-        if (task >= A->ntasks) break;
+        const uint32_t id = uni(next);
+        if (id >= A->ntasks) break;
         next = 0;
-        if (flags & kFusedStatic) next = task + nwaves;
+        if (flags & kFusedStatic) next = id + nwaves;
         else if (flags & kFusedPrefetch) next = dequeue();
+        // guided tail: ids from nbig on are pieces pp of np of their task
+        uint32_t task = id, pp = 0, np = 1;
+        if (id >= nbig) {
+            const uint32_t q = (id - nbig) / nparts;
+            pp = id - nbig - q * nparts;
+            np = nparts;
+            task = nbig + q;
+        }
         uint32_t i = 0;
         while (i + 1 < A->nseg && task >= A->segs[i].task_end) ++i;
         const FusedSeg S_ = A->segs[i];  // scalar loads of one descriptor
@@ -170,8 +200,8 @@ DEV void fused_body(FusedArgsK* A) {
             HM_FUSED_CASE_S(13, true)
             HM_FUSED_CASE_S(14, true)
             HM_FUSED_CASE_S(15, true)
-            case kVarChained: fused_chained<CSUM>(A, S_, k, best, sums); break;
-            default: fused_generic<CSUM>(A, S_, k, best, sums); break;
+            case kVarChained: fused_chained<CSUM>(A, S_, k, pp, np, best, sums); break;
+            default: fused_generic<CSUM>(A, S_, k, pp, np, best, sums); break;
         }
         if (!(flags & (kFusedPrefetch | kFusedStatic))) next = dequeue();
     }

@@ -151,9 +151,13 @@ __global__ void __launch_bounds__(kBlock) hm_fused_plan_kernel(const FusedPlanAr
 // ---------------------------------------------------------------------------
 // Second reduce pass and init
 // ---------------------------------------------------------------------------
+// `host`, when set, is pinned fine-grained host memory (the call's 16-B
+// readback slot): the result is also stored there with system-scope vector
+// stores, so the host reads it once the stream is done -- no device-to-host
+// copy (a blit kernel and a launch gap) after the fold.
 __global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restrict__ cand,
                                                          uint32_t n, uint32_t stride,
-                                                         uint64_t* best) {
+                                                         uint64_t* best, uint64_t* host) {
     __shared__ uint64_t sk[kBlock / kWaveSize], sn[kBlock / kWaveSize];
     uint64_t k = ~0ull, nn = ~0ull;
     if (threadIdx.x == 0) { k = best[0]; nn = best[1]; }
@@ -169,6 +173,11 @@ __global__ void __launch_bounds__(kBlock) hm_fold_kernel(const uint64_t* __restr
             if (sk[w] < k || (sk[w] == k && sn[w] < nn)) { k = sk[w]; nn = sn[w]; }
         best[0] = k;
         best[1] = nn;
+        if (host) {
+            __hip_atomic_store(&host[0], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&host[1], nn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+        }
     }
 }
 
@@ -221,8 +230,8 @@ hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base
 }
 
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
-                       uint32_t stride) {
-    hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, stride, best);
+                       uint32_t stride, uint64_t* host) {
+    hipLaunchKernelGGL(hm_fold_kernel, dim3(1), dim3(kBlock), 0, s, cand, n, stride, best, host);
     return hipGetLastError();
 }
 

@@ -120,7 +120,11 @@ constexpr int kMaxFusedSegs = 20;          // digit counts of a u64 nonce
 constexpr uint64_t kFusedNonces = 1ull << 27;  // requests up to this size are fused
 constexpr uint32_t kFusedKwRows = 12288;   // chained K+W rows per stream (f <= 4: <= 11110)
 constexpr uint32_t kFusedAuxWords = kFusedKwRows * 64 + kMaxFusedSegs * 164;
-constexpr uint32_t kFusedChainedPiece = 100;  // loop values per chained task
+// loop values per chained task: block 0 once per 100 values (C_eff 1.01).
+// 1000 would amortise it 10x better, but a fused request (<= 2^27 nonces)
+// then has fewer than 2^27 / 64000 = 2097 chained tasks, not one per wave of
+// the grid (3072): the launch would run part-empty.
+constexpr uint32_t kFusedChainedPiece = 100;
 // variant ids: tiled W1 * 4 + 2 * straddle + trailer (4..63), then:
 constexpr uint32_t kVarChained = 64;
 constexpr uint32_t kVarGeneric = 65;
@@ -150,6 +154,11 @@ constexpr uint32_t kFusedPrefetch = 2;     // dequeue the next task id while run
 constexpr uint32_t kFusedStatic = 4;       // no queue: wave w runs tasks w, w + nwaves, w + 2 nwaves, ...
 constexpr uint32_t kFusedLds = 8;          // dequeue through the workgroup's LDS dispenser (scan_tasks.hpp)
 
+// Guided tail of the fused launch (round 6): task ids below `nbig` run one
+// whole task each; the last ~one wave-round of tasks (the cheapest layouts,
+// queued last) is split into `nparts` pieces each, ids nbig + i*nparts + p,
+// so the waves that finish early share the end and the launch's tail is a
+// piece, not a task (HM_OPT_FUSED_TAIL).
 struct FusedArgs {
     const uint32_t* rec;
     const uint32_t* aux;
@@ -157,6 +166,8 @@ struct FusedArgs {
     uint64_t* cand;
     uint64_t* sums;       // checked scans only
     uint32_t ntasks, nseg;
+    uint32_t nbig;        // ids below run whole tasks
+    uint32_t nparts;      // pieces per split task (1, 2, 5, 10)
     uint32_t flags;       // kFused*
     uint32_t r;           // prefix-remainder bytes (generic)
     uint32_t pw[16];      // prefix remainder words (generic)
@@ -199,9 +210,10 @@ hipError_t launch_sum_fold(const uint64_t* sums, uint32_t n, uint64_t* acc, hipS
 hipError_t launch_kw_table(uint32_t* out, uint32_t f, uint32_t fe, uint64_t base,
                            uint64_t total_bits, hipStream_t s);
 // Fold n (key, nonce) pairs (pair i at cand + 2*i*stride) plus *best into
-// *best (lexicographic min).
+// *best (lexicographic min); with `host` (pinned fine-grained host memory)
+// the result is also written there, system-scope.
 hipError_t launch_fold(const uint64_t* cand, uint32_t n, uint64_t* best, hipStream_t s,
-                       uint32_t stride = 1);
+                       uint32_t stride = 1, uint64_t* host = nullptr);
 hipError_t launch_init_best(uint64_t* best, uint32_t n, hipStream_t s);
 // The fused launch's planner: tile records, tables, counter/result/acc reset.
 hipError_t launch_fused_plan(const FusedPlanArgs& a, hipStream_t s);

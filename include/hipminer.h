@@ -204,6 +204,23 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */
+#define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 5; ABI 1.8): the last
+                                  ~one wave-round of a fused launch's tasks
+                                  (the cheapest layouts, queued last) runs as
+                                  this many pieces each, so waves that finish
+                                  early share the end of the launch; 1 = no
+                                  split                                        */
+#define HM_OPT_TAIL_FUSED 15    /* 1 (default; ABI 1.8): the segments of a large
+                                  request that its dominant kernel does not run
+                                  (bradfitz [0, 2^32): d <= 8) go into ONE fused
+                                  launch on a low-priority stream, in the
+                                  dominant launch's tail, when they fit one; 0:
+                                  one launch per segment on the tail streams */
+#define HM_OPT_HOST_RESULT 16   /* experiment hook (0/1, default 1; ABI 1.8): the
+                                  call's last fold kernel stores the 16-B
+                                  results into pinned host memory (system-scope
+                                  stores), so no device-to-host copy follows;
+                                  0: hipMemcpyAsync readback as before 1.8    */
 #define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
                                   a call blocks until its GPU work is done; > 0 =
                                   a call returns HM_ERR_TIMEOUT (and abandons the

@@ -174,3 +174,87 @@ def test_task_dispensing_flags_checked(ctx, oracle_mod, flags):
             assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
     finally:
         ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, 1)
+
+
+@pytest.mark.parametrize("tail", [1, 2, 10])
+def test_guided_tail_pieces_checked(ctx, oracle_mod, tail):
+    """HM_OPT_FUSED_TAIL (round 6; default 5, covered by every other test): the
+    last ~one wave-round of a fused launch's tasks run as `tail` pieces each
+    -- tiled, trailer, chained and generic tasks alike, combined with split
+    tiled tasks and every dispensing mode -- and every nonce is still hashed
+    exactly once: (min, key sum, count) equal the oracle's."""
+    rng = random.Random(1000 + tail)
+    ctx.set_option(_lib.HM_OPT_FUSED_TAIL, tail)
+    try:
+        assert ctx.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+        for L in (0, 8, 45, 55, 57, 60, 61, 100, 120):
+            m = bytes(rng.randrange(33, 127) for _ in range(L))
+            for lo, hi in ((max(0, 10**rng.randrange(3, 19) - rng.randrange(1, 400_000)), None),
+                           (0, 20_000), (10**15, 10**15 + 3)):
+                hi = hi if hi is not None else lo + rng.randrange(1, 2_000_000)
+                assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), \
+                    (tail, L, lo, hi)
+                assert ctx.stats()["dom_kind"] == _lib.HM_KIND_FUSED
+        for parts, flags in ((2, 1), (5, 9), (1, 4), (1, 2)):
+            ctx.set_option(_lib.HM_OPT_FUSED_PARTS, parts)
+            ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, flags)
+            m = b"thom yorke"
+            assert ctx.scan_checked(m, 10**9 - 900_000, 10**9 + 900_000) == \
+                oracle_mod.c_scan_sum(m, 10**9 - 900_000, 10**9 + 900_000), (parts, flags)
+    finally:
+        ctx.set_option(_lib.HM_OPT_FUSED_PARTS, 1)
+        ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, 1)
+        ctx.set_option(_lib.HM_OPT_FUSED_TAIL, 5)
+
+
+def test_fused_tail_option_validated(ctx):
+    for bad in (0, 3, 4, 11, -1):
+        with pytest.raises(_lib.HipMinerError):
+            ctx.set_option(_lib.HM_OPT_FUSED_TAIL, bad)
+
+
+def test_large_request_tail_segments_fused(ctx, oracle_mod):
+    """HM_OPT_TAIL_FUSED (round 6, default on): a large request's segments off
+    its dominant kernel (here d <= 8 of [0, 3*10^8], 10^8 nonces) run as ONE
+    fused launch in the dominant launch's tail.  Checked against the oracle
+    with the coverage sums, on 2 and 4 streams, and equal to the per-segment
+    tail (option off); configs[1] and [2] keep their fixtures."""
+    m, lo, hi = b"bradfitz", 0, 3 * 10**8
+    exp = oracle_mod.fast_scan_sum(m, lo, hi) if oracle_mod.fast_available() else \
+        oracle_mod.c_scan_sum(m, lo, hi)
+    for streams in (2, 4):
+        ctx.set_option(_lib.HM_OPT_STREAMS, streams)
+        try:
+            assert ctx.scan_checked(m, lo, hi) == exp, streams
+            st = ctx.stats()
+            assert st["dom_kind"] == _lib.HM_KIND_TILED, st
+            # the dominant launch(es), then ONE fused launch for d = 1..8
+            assert st["launches"] == st["dom_launches"] + 1, st
+            ctx.set_option(_lib.HM_OPT_TAIL_FUSED, 0)
+            assert ctx.scan_checked(m, lo, hi) == exp, streams
+            assert ctx.stats()["launches"] == st["dom_launches"] + 8
+        finally:
+            ctx.set_option(_lib.HM_OPT_TAIL_FUSED, 1)
+            ctx.set_option(_lib.HM_OPT_STREAMS, 4)
+    assert ctx.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+    import bench
+    assert ctx.scan(bench.long120(), 0, 2**32 - 1) == (1410660608, 124104753)
+
+
+def test_results_stored_to_host_or_copied_agree(oracle_mod):
+    """HM_OPT_HOST_RESULT (round 6, default on): the call's last fold kernel
+    stores the 16-B results in pinned host memory; with the option off they
+    are copied back as before.  Same answers on one device, a batch, a
+    two-device host merge and the RCCL merge."""
+    reqs = [(b"bradfitz", 0, 10**7 + 1), (b"thom yorke", 10**9, 10**9 + 2 * 10**8),
+            (b"x" * 120, 0, 99_999), (b"", 5, 4)]
+    exp = [oracle_mod.c_scan(m, a, b) if a <= b else (MAX, 0) for m, a, b in reqs]
+    for devs, rccl in (([0], False), ([0, 0], False), ([0], True)):
+        with _lib.Context(devs) as c:
+            if rccl:
+                c.set_option(_lib.HM_OPT_MERGE_RCCL, 1)
+            for host in (1, 0, 1):
+                c.set_option(_lib.HM_OPT_HOST_RESULT, host)
+                assert c.scan_many(reqs) == exp, (devs, rccl, host)
+                for (m, a, b), e in zip(reqs, exp):
+                    assert c.scan(m, a, b) == e, (devs, rccl, host, m, a, b)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round-6 run b: the fused-launch changes (guided tail pieces, a large
+# request's tail segments as one fused launch, results stored to pinned host
+# memory) -- their GPU tests first, then interleaved A/Bs of each option on
+# configs[0]'s request, the 120-B message at 10^7, cfg2 and cfg3.
+set -o pipefail
+export TMPDIR=/tmp
+O=${1:-gpurun_out/r06b}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_enqueue.py tests/test_gpu_deadline.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_fused.log 2>&1
+prc=$?
+tail -3 $O/pytest_fused.log
+if [ $prc -gt 1 ]; then echo "pytest rc=$prc: stopping"; exit $prc; fi
+A="timeout -k 10 240 python -u tools/ab_opts.py"
+$A 300 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 t2:FUSED_TAIL=2 t10:FUSED_TAIL=10 -- bradfitz 0 10000001 > $O/ab_tail_cfg1.jsonl 2> $O/ab.err &&
+$A 300 h1:HOST_RESULT=1 h0:HOST_RESULT=0 poll:DEADLINE_MS=60000 h0poll:HOST_RESULT=0,DEADLINE_MS=60000 -- bradfitz 0 10000001 > $O/ab_host_cfg1.jsonl 2>> $O/ab.err &&
+$A 300 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 t2:FUSED_TAIL=2 t10:FUSED_TAIL=10 -- long120 0 10000000 > $O/ab_tail_long120_1e7.jsonl 2>> $O/ab.err &&
+$A 300 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 -- bradfitz 0 1000000 > $O/ab_tail_1e6.jsonl 2>> $O/ab.err &&
+$A 60 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 t10:FUSED_TAIL=10 -- bradfitz 0 99999999 > $O/ab_tail_1e8.jsonl 2>> $O/ab.err &&
+$A 15 s2f:STREAMS=2 s2n:STREAMS=2,TAIL_FUSED=0 s4f:STREAMS=4 s4n:STREAMS=4,TAIL_FUSED=0 > $O/ab_tailseg_cfg2.jsonl 2>> $O/ab.err &&
+$A 15 s2f:STREAMS=2 s2n:STREAMS=2,TAIL_FUSED=0 s4f:STREAMS=4 s4n:STREAMS=4,TAIL_FUSED=0 -- long120 0 4294967295 > $O/ab_tailseg_cfg3.jsonl 2>> $O/ab.err
+rc=$?
+cat $O/ab_*.jsonl | cut -c1-230
+echo "final rc=$rc"
+exit $rc
