@@ -132,9 +132,12 @@ def hot_loop(insts, heads):
     return best
 
 
-def all_loops(insts, heads):
+def all_loops(insts, heads, latch_bytes=None):
     """Every innermost loop with >= MIN_LOOP instructions, in address order
-    (the fused kernel holds one hot loop per segment layout)."""
+    (the fused kernel holds one hot loop per segment layout).  latch_bytes:
+    how far before its header a loop's latch block may start (LATCH_BYTES;
+    checks of already placed code pass more, since re-encoding grows it)."""
+    latch = LATCH_BYTES if latch_bytes is None else latch_bytes
     out = []
     addr_index = {x[0]: i for i, x in enumerate(insts)}
     for k in heads:
@@ -142,7 +145,7 @@ def all_loops(insts, heads):
             continue
         head = insts[k][0]
         ends = [(i, x[3]) for i, x in enumerate(insts)
-                if i > k and x[3] is not None and head - LATCH_BYTES <= x[3] <= head]
+                if i > k and x[3] is not None and head - latch <= x[3] <= head]
         if not ends:
             continue
         end, target = max(ends)
@@ -158,11 +161,11 @@ def all_loops(insts, heads):
     return keep
 
 
-def kernel_loops(sym, insts, heads):
+def kernel_loops(sym, insts, heads, latch_bytes=None):
     """The loops the pass places: every hot loop of the fused kernels, the
     single hottest loop of every other kernel."""
     if "fused" in sym:
-        return all_loops(insts, heads)
+        return all_loops(insts, heads, latch_bytes)
     lp = hot_loop(insts, heads)
     return [lp] if lp else []
 
