@@ -37,6 +37,7 @@ HM_OPT_DEADLINE_MS = 13
 HM_OPT_FUSED_TAIL = 14
 HM_OPT_TAIL_FUSED = 15
 HM_OPT_HOST_RESULT = 16
+HM_OPT_QUEUE_BATCH = 17
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 

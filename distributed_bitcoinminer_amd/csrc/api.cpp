@@ -57,6 +57,12 @@ constexpr uint64_t kConcurrentNonces = 1ull << 27;
 constexpr int kFusedPerCu = 3;
 constexpr uint32_t kFusedDefaultFlags = kFusedStaticFirst;
 constexpr uint32_t kFusedDefaultParts = 1;  // tiled fused tasks: one tens digit (10 steps)
+// Tasks one queue atomic fetches for a workgroup (scan_tasks.hpp lds_dequeue,
+// log2): 4, and 16 for launches of at least kBigLaunchNonces nonces
+// (HM_OPT_QUEUE_BATCH; configs[3]'s d = 12 launch: 9e11 nonces, ~24 s).
+constexpr uint32_t kQueueShift = 2;
+constexpr uint32_t kQueueShiftBig = 4;
+constexpr uint64_t kBigLaunchNonces = 100000000000ull;
 // Guided tail of a fused launch (HM_OPT_FUSED_TAIL): the last ~one wave-round
 // of tasks is cut into this many pieces each.
 constexpr uint32_t kFusedDefaultTail = 5;
@@ -162,6 +168,7 @@ struct hm_ctx {
     uint32_t fused_tail = kFusedDefaultTail;    // HM_OPT_FUSED_TAIL (1 = no split)
     bool tail_fused = true;  // HM_OPT_TAIL_FUSED: a large request's tail segments in one fused launch
     bool host_result = true; // HM_OPT_HOST_RESULT: results stored to pinned host memory by the last fold
+    int queue_batch = 0;     // HM_OPT_QUEUE_BATCH: 0 = auto, else tasks per queue atomic (4..32)
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -317,6 +324,12 @@ int launch_scan(const Device::Fn& f, const Args& args, int grid, hipStream_t st)
                    HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
     HIPCHK(hipModuleLaunchKernel(f.fn, (unsigned)grid, 1, 1, kBlock, 1, 1, 0, st, nullptr, cfg));
     return HM_OK;
+}
+
+// log2 of the tasks per queue atomic of a per-segment launch over `nonces`.
+uint32_t queue_shift(const hm_ctx* ctx, uint64_t nonces) {
+    if (ctx->queue_batch > 0) return (uint32_t)__builtin_ctz((unsigned)ctx->queue_batch);
+    return nonces >= kBigLaunchNonces ? kQueueShiftBig : kQueueShift;
 }
 
 uint32_t count_compressions(const SegPlan& s) {
@@ -515,6 +528,7 @@ int launch_chained_tiles(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPl
     ca.tch = s.tch;
     ca.vmax = (uint32_t)(pow10_u64(s.q) - 1);
     ca.q = s.q;
+    ca.lds_shift = queue_shift(ctx, tile_span_nonces(s, t, nt) / nep);
     const Device::Fn* fn = nullptr;
     int rc = scan_fn(dv, chained_symbol(ctx->csum), &fn);
     if (rc) return rc;
@@ -626,6 +640,7 @@ int enqueue_segment(hm_ctx* ctx, Device& dv, const MsgPlan& mp, const SegPlan& s
             ta.q = s.q;
             ta.lane_shift = s.lane_shift;
             ta.loop_shift = s.loop_shift;
+            ta.lds_shift = queue_shift(ctx, tile_span_nonces(s, t, nt));
             memcpy(ta.trailer_kw, kw, sizeof kw);
             tiled_loop_sigma0(s, ta.s0_loop);
             const Device::Fn* fn = nullptr;
@@ -1345,6 +1360,11 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
         case HM_OPT_FUSED_PARTS:
             if (value != 1 && value != 2 && value != 5 && value != 10) return HM_ERR_INVALID;
             ctx->fused_parts = (uint32_t)value;
+            return HM_OK;
+        case HM_OPT_QUEUE_BATCH:
+            if (value != 0 && value != 4 && value != 8 && value != 16 && value != 32)
+                return HM_ERR_INVALID;
+            ctx->queue_batch = (int)value;
             return HM_OK;
         case HM_OPT_HOST_RESULT:
             ctx->host_result = value != 0;

@@ -60,6 +60,7 @@ struct TiledArgs {
     uint32_t q;          // lane digits
     uint32_t lane_shift; // bit offset of the lowest lane digit in the (W[W1-1]:W[W1]) pair
     uint32_t loop_shift; // bit offset of the units loop digit (tens digit at +8)
+    uint32_t lds_shift;  // log2 of the tasks one queue atomic fetches (scan_tasks.hpp lds_dequeue)
     uint32_t trailer_kw[64];  // K[i]+W[i] of the constant trailer block (TRAILER only)
     uint32_t s0_loop[100];    // sigma0 of the loop-digit part of W[W1], index t1*10+t0
 };
@@ -93,6 +94,7 @@ struct ChainedArgs {
     uint32_t vmax;           // 10^q - 1
     uint32_t q;              // lane digits (<= 5: W15 and the last byte of W14)
     uint32_t nloop;          // loop values per lane value and epoch = table rows = 10^fe
+    uint32_t lds_shift;      // log2 of the tasks one queue atomic fetches
 };
 
 // Generic scan: one nonce per lane (small / irregular segments, cross-checks).

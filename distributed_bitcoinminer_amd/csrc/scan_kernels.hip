@@ -55,7 +55,7 @@ DEV void tiled_body(const TiledArgs& A) {
     lds_queue_init(&queue);
 
     for (;;) {
-        const uint32_t task = lds_dequeue(&queue, A.counter);
+        const uint32_t task = lds_dequeue(&queue, A.counter, A.lds_shift);
         if (task >= A.ntasks) break;
         // guided sizes: whole units first, then tenths (one tens digit each)
         uint32_t unit = task, t1_begin = 0, t1_end = 10;
@@ -102,7 +102,7 @@ DEV void chained_body(const ChainedArgs& A) {
     lds_queue_init(&queue);
 
     for (;;) {
-        const uint32_t task = lds_dequeue(&queue, A.counter);
+        const uint32_t task = lds_dequeue(&queue, A.counter, A.lds_shift);
         if (task >= A.ntasks) break;
         // guided sizes: whole loop chunks first, then kSplit pieces of each
         uint32_t unit = task, part = 0, nparts = 1;

@@ -62,9 +62,13 @@ DEV void take_step(WaveBest& best, bool cand, uint32_t h0, uint32_t h1, uint64_t
 // execute memory-side (PMC WRITE_SIZE per cfg2 launch 18.1 -> 4.6 MB; cfg2
 // +0.1 %, cfg3 +1.0 %, d = 12 +0.04 % in an interleaved A/B,
 // profiles/r05/experiments/lds_dispenser/).  The ring cannot be lapped: a
-// batch's slot is rewritten only 16 tickets later, and each of the 4 waves
-// holds one ticket at a time.
+// batch's slot is rewritten only 4 batches (>= 16 tickets) later, and each
+// of the 4 waves holds one ticket at a time.  The batch is 2^shift tasks:
+// kLdsBatch by default; launches of >= 10^11 nonces (configs[3]'s d = 12
+// segment) take 16 (round 6, HM_OPT_QUEUE_BATCH), since a tail imbalance of
+// 16 tenth-units is nothing against their seconds of work.
 constexpr uint32_t kLdsBatch = 4;
+constexpr uint32_t kLdsShift = 2;  // log2(kLdsBatch)
 struct LdsQueue {
     uint32_t ticket;
     uint32_t base[4];
@@ -77,13 +81,13 @@ DEV void lds_queue_init(LdsQueue* q) {
     }
     __syncthreads();
 }
-DEV uint32_t lds_dequeue(LdsQueue* q, unsigned int* counter) {
+DEV uint32_t lds_dequeue(LdsQueue* q, unsigned int* counter, uint32_t shift = kLdsShift) {
     uint32_t task = 0;
     if (__lane_id() == 0) {
         const uint32_t t = atomicAdd(&q->ticket, 1u);
-        const uint32_t batch = t / kLdsBatch, slot = batch & 3u;
-        if (t - batch * kLdsBatch == 0) {
-            q->base[slot] = atomicAdd(counter, kLdsBatch);
+        const uint32_t batch = t >> shift, slot = batch & 3u;
+        if (t - (batch << shift) == 0) {
+            q->base[slot] = atomicAdd(counter, 1u << shift);
             __hip_atomic_store(&q->ready[slot], batch + 1, __ATOMIC_RELEASE,
                                __HIP_MEMORY_SCOPE_WORKGROUP);
         } else {
@@ -91,7 +95,7 @@ DEV uint32_t lds_dequeue(LdsQueue* q, unsigned int* counter) {
                                      __HIP_MEMORY_SCOPE_WORKGROUP) != batch + 1)
                 __builtin_amdgcn_s_sleep(2);
         }
-        task = q->base[slot] + (t - batch * kLdsBatch);
+        task = q->base[slot] + (t - (batch << shift));
     }
     return uni(task);
 }

@@ -221,6 +221,10 @@ typedef struct hm_stats {
                                   results into pinned host memory (system-scope
                                   stores), so no device-to-host copy follows;
                                   0: hipMemcpyAsync readback as before 1.8    */
+#define HM_OPT_QUEUE_BATCH 17   /* experiment hook (0, 4, 8, 16, 32; ABI 1.8):
+                                  tasks a workgroup fetches per work-queue
+                                  atomic in the per-segment kernels; 0 (default)
+                                  = 4, and 16 for launches of >= 10^11 nonces */
 #define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
                                   a call blocks until its GPU work is done; > 0 =
                                   a call returns HM_ERR_TIMEOUT (and abandons the

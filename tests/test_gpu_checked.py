@@ -210,3 +210,22 @@ def test_checked_empty_and_edges(ctx):
     assert ctx.scan_checked(b"bradfitz", 5, 4) == ((MAX, 0), 0, 0)
     assert ctx.scan_checked(b"bradfitz", MAX, MAX) == ((_lib.host_hash(b"bradfitz", MAX), MAX),
                                                         _lib.host_hash(b"bradfitz", MAX), 1)
+
+
+@pytest.mark.parametrize("batch", [4, 32])
+def test_queue_batch_checked(ctx, oracle_mod, batch):
+    """HM_OPT_QUEUE_BATCH (round 6): a workgroup fetching 4 or 32 tasks per
+    queue atomic still hashes every nonce once -- tiled (plain and straddle)
+    and chained launches with their guided tails, checked against the
+    oracle's (min, key sum, count).  The default (auto) takes 16 for
+    launches of >= 10^11 nonces, which test_gpu_full_size covers."""
+    ctx.set_option(_lib.HM_OPT_QUEUE_BATCH, batch)
+    ctx.set_option(_lib.HM_OPT_FUSED, 0)
+    try:
+        for m, lo, hi in ((b"bradfitz", 0, 3 * 10**6), (b"thom yorke", 10**9 - 10**6, 10**9 + 10**6),
+                          (b"z" * 120, 10**7 - 10**6, 10**7 + 10**6),
+                          (b"q" * 60, 10**10, 10**10 + 2 * 10**6)):
+            assert ctx.scan_checked(m, lo, hi) == oracle_mod.c_scan_sum(m, lo, hi), (batch, m, lo)
+    finally:
+        ctx.set_option(_lib.HM_OPT_QUEUE_BATCH, 0)
+        ctx.set_option(_lib.HM_OPT_FUSED, 1)

@@ -7,7 +7,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=${1:-gpurun_out/r06b}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_enqueue.py tests/test_gpu_deadline.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_fused.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fused.py tests/test_gpu_enqueue.py tests/test_gpu_deadline.py tests/test_gpu_parity.py tests/test_gpu_checked.py -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_fused.log 2>&1
 prc=$?
 tail -3 $O/pytest_fused.log
 if [ $prc -gt 1 ]; then echo "pytest rc=$prc: stopping"; exit $prc; fi
@@ -19,6 +19,12 @@ $A 300 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 -- bradfitz 0 1000000 > $O/ab_tail_1e6.js
 $A 60 t5:FUSED_TAIL=5 t1:FUSED_TAIL=1 t10:FUSED_TAIL=10 -- bradfitz 0 99999999 > $O/ab_tail_1e8.jsonl 2>> $O/ab.err &&
 $A 15 s2f:STREAMS=2 s2n:STREAMS=2,TAIL_FUSED=0 s4f:STREAMS=4 s4n:STREAMS=4,TAIL_FUSED=0 > $O/ab_tailseg_cfg2.jsonl 2>> $O/ab.err &&
 $A 15 s2f:STREAMS=2 s2n:STREAMS=2,TAIL_FUSED=0 s4f:STREAMS=4 s4n:STREAMS=4,TAIL_FUSED=0 -- long120 0 4294967295 > $O/ab_tailseg_cfg3.jsonl 2>> $O/ab.err
+ &&
+$A 4 qa:QUEUE_BATCH=0 q4:QUEUE_BATCH=4 -- bradfitz 100000000000 299999999999 > $O/ab_queue_d12.jsonl 2>> $O/ab.err &&
+$A 15 qa:QUEUE_BATCH=0 q4:QUEUE_BATCH=4 > $O/ab_queue_cfg2.jsonl 2>> $O/ab.err &&
+P="timeout -s KILL 90 rocprofv3 --kernel-trace" &&
+$P --pmc WRITE_SIZE -d $O/pmc_write_d12_auto -o run --output-format csv -- python tools/quick_scan.py bradfitz 100000000000 299999999999 1 > $O/pmc_write_d12_auto.log 2>&1 &&
+$P --pmc WRITE_SIZE -d $O/pmc_write_d12_q4 -o run --output-format csv -- python tools/quick_scan.py bradfitz 100000000000 299999999999 1 --opt QUEUE_BATCH=4 > $O/pmc_write_d12_q4.log 2>&1
 rc=$?
 cat $O/ab_*.jsonl | cut -c1-230
 echo "final rc=$rc"

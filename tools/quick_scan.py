@@ -7,6 +7,12 @@ if "--lib" in sys.argv:  # an experiment build (tools/build_variant.sh)
     _lib.LIB_PATH = sys.argv[i + 1]
     del sys.argv[i:i + 2]
 c = _lib.Context([0])
+if "--opt" in sys.argv:  # --opt NAME=VALUE (an HM_OPT_* suffix), repeatable
+    while "--opt" in sys.argv:
+        i = sys.argv.index("--opt")
+        k, _, v = sys.argv[i + 1].partition("=")
+        c.set_option(getattr(_lib, "HM_OPT_" + k), int(v))
+        del sys.argv[i:i + 2]
 msg = sys.argv[1].encode() if len(sys.argv) > 1 else b"bradfitz"
 lo = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 hi = int(sys.argv[3]) if len(sys.argv) > 3 else 2**32 - 1
