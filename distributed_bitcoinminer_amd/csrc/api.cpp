@@ -63,9 +63,9 @@ constexpr uint32_t kFusedDefaultParts = 1;  // tiled fused tasks: one tens digit
 constexpr uint32_t kQueueShift = 2;
 constexpr uint32_t kQueueShiftBig = 4;
 constexpr uint64_t kBigLaunchNonces = 100000000000ull;
-// Guided tail of a fused launch (HM_OPT_FUSED_TAIL): the last ~one wave-round
-// of tasks is cut into this many pieces each.
-constexpr uint32_t kFusedDefaultTail = 5;
+// Guided tail of a fused launch (HM_OPT_FUSED_TAIL): the tasks of the last,
+// partial wave-round are cut into up to this many pieces each.
+constexpr uint32_t kFusedDefaultTail = 10;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -858,15 +858,22 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
         ce_base[i] = ce;
         seg_cnt[i] = cnt;
     }
-    // guided tail: the last min(tasks, one wave-round of the occupancy grid)
-    // tasks -- the cheapest layouts, queued last -- run as fused_tail pieces
-    // each (the grid is then sized by ids, pieces included)
+    // guided tail: waves that start together on equal tasks finish their
+    // rounds together, so the launch ends on a partial round of
+    // tasks mod waves tasks, with most of the GPU idle for a whole task's
+    // time.  Those last tasks (the cheapest layouts, queued last) run as
+    // pieces instead: the most pieces each (<= fused_tail; 10, 5, 2) that
+    // still fit one round of the grid.  Splitting more (a whole round) costs
+    // more than it saves: every piece is one more atomic on the launch's one
+    // queue counter, which saturates (profiles/r06/experiments/fused_tail/).
     const uint64_t cap_waves =
         (uint64_t)persistent_grid(ctx, dv, kFusedPerCu, 1ull << 40) * (kBlock / kWaveSize);
-    const uint32_t nparts = ctx->fused_tail;
-    const uint64_t nsplit = nparts > 1 ? std::min<uint64_t>(tasks, cap_waves) : 0;
-    const uint64_t nbig = tasks - nsplit;
-    const uint64_t ids = nbig + nsplit * nparts;
+    const uint64_t nsplit = tasks % cap_waves;
+    uint32_t nparts = 1;
+    for (uint32_t p : {10u, 5u, 2u})
+        if (p <= ctx->fused_tail && nsplit * p <= cap_waves) { nparts = p; break; }
+    const uint64_t nbig = nparts > 1 ? tasks - nsplit : tasks;
+    const uint64_t ids = nbig + (nparts > 1 ? nsplit * nparts : 0);
     if (ids >= (1ull << 31) || jobs >= (1ull << 31) || aux_next > kFusedAuxWords)
         return HM_ERR_INTERNAL;  // excluded by fusible()
     double comp_w = 0;  // executed compressions x nonces (hm_stats)
@@ -874,7 +881,8 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
         double ce = ce_base[i];
         if (seg_units[i] > 0) {  // chained: block 0 per task, and per piece of a split task
             const uint64_t a = i ? fa.segs[i - 1].task_end : 0, b = fa.segs[i].task_end;
-            const uint64_t split = b > std::max(a, nbig) ? b - std::max(a, nbig) : 0;
+            const uint64_t split =
+                nparts > 1 && b > std::max(a, nbig) ? b - std::max(a, nbig) : 0;
             ce += (double)(b - a + split * (nparts - 1)) / seg_units[i];
         }
         comp_w += ce * (double)seg_cnt[i];

@@ -157,10 +157,10 @@ constexpr uint32_t kFusedStatic = 4;       // no queue: wave w runs tasks w, w +
 constexpr uint32_t kFusedLds = 8;          // dequeue through the workgroup's LDS dispenser (scan_tasks.hpp)
 
 // Guided tail of the fused launch (round 6): task ids below `nbig` run one
-// whole task each; the last ~one wave-round of tasks (the cheapest layouts,
-// queued last) is split into `nparts` pieces each, ids nbig + i*nparts + p,
-// so the waves that finish early share the end and the launch's tail is a
-// piece, not a task (HM_OPT_FUSED_TAIL).
+// whole task each; the tasks of the last, partial wave-round (the cheapest
+// layouts, queued last) are split into `nparts` pieces each, ids nbig +
+// i*nparts + p, so that round fills the grid and lasts a piece, not a task
+// (HM_OPT_FUSED_TAIL).
 struct FusedArgs {
     const uint32_t* rec;
     const uint32_t* aux;

@@ -204,11 +204,13 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */
-#define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 5; ABI 1.8): the last
-                                  ~one wave-round of a fused launch's tasks
-                                  (the cheapest layouts, queued last) runs as
-                                  this many pieces each, so waves that finish
-                                  early share the end of the launch; 1 = no
+#define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 10; ABI 1.8): the tasks
+                                  of a fused launch's last, partial wave-round
+                                  (tasks mod waves; the cheapest layouts, queued
+                                  last) run as up to this many pieces each --
+                                  as many as still fit one round of the grid --
+                                  so the launch does not end on a round of
+                                  whole tasks with most waves idle; 1 = no
                                   split                                        */
 #define HM_OPT_TAIL_FUSED 15    /* 1 (default; ABI 1.8): the segments of a large
                                   request that its dominant kernel does not run

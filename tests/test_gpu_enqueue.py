@@ -145,6 +145,10 @@ def test_streams_are_made_on_first_use(oracle_mod):
         assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
         assert c.streams_made() == 2
         c.set_option(_lib.HM_OPT_STREAMS, 4)
+        # the tail segments (d <= 8) run as one fused launch: 2 streams suffice
+        assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+        assert c.streams_made() == 2
+        c.set_option(_lib.HM_OPT_TAIL_FUSED, 0)  # one launch per tail segment
         assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
         assert c.streams_made() == 4
     with _lib.Context([0]) as c:

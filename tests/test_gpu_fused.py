@@ -176,13 +176,13 @@ def test_task_dispensing_flags_checked(ctx, oracle_mod, flags):
         ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, 1)
 
 
-@pytest.mark.parametrize("tail", [1, 2, 10])
+@pytest.mark.parametrize("tail", [1, 2, 5])
 def test_guided_tail_pieces_checked(ctx, oracle_mod, tail):
-    """HM_OPT_FUSED_TAIL (round 6; default 5, covered by every other test): the
-    last ~one wave-round of a fused launch's tasks run as `tail` pieces each
-    -- tiled, trailer, chained and generic tasks alike, combined with split
-    tiled tasks and every dispensing mode -- and every nonce is still hashed
-    exactly once: (min, key sum, count) equal the oracle's."""
+    """HM_OPT_FUSED_TAIL (round 6; default 10, covered by every other test):
+    the tasks of a fused launch's last partial wave-round run as up to `tail`
+    pieces each -- tiled, trailer, chained and generic tasks alike, combined
+    with split tiled tasks and every dispensing mode -- and every nonce is
+    still hashed exactly once: (min, key sum, count) equal the oracle's."""
     rng = random.Random(1000 + tail)
     ctx.set_option(_lib.HM_OPT_FUSED_TAIL, tail)
     try:
@@ -204,7 +204,7 @@ def test_guided_tail_pieces_checked(ctx, oracle_mod, tail):
     finally:
         ctx.set_option(_lib.HM_OPT_FUSED_PARTS, 1)
         ctx.set_option(_lib.HM_OPT_FUSED_FLAGS, 1)
-        ctx.set_option(_lib.HM_OPT_FUSED_TAIL, 5)
+        ctx.set_option(_lib.HM_OPT_FUSED_TAIL, 10)
 
 
 def test_fused_tail_option_validated(ctx):

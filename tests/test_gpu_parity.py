@@ -272,11 +272,13 @@ def test_stats_accounting(ctx):
     # counted exactly (ABI 1.5): one block-0 compression per task and lane;
     # whole units cost 1/1000 per loop value, guided-split ones 10/1000
     assert 1.001 <= st["dom_compressions_eff"] <= 1.01
-    # the fused launch: chained tasks of 100 loop values (block 0 per 100)
+    # the fused launch: chained tasks of 100 loop values (block 0 per 100),
+    # plus one block 0 per piece of the guided tail's split tasks (the last
+    # partial wave-round: 15625 mod 3072 tasks x 10 pieces on 256 CUs)
     ctx.scan(long120, 10**9, 10**9 + 10**8)
     st = ctx.stats()
     assert st["dom_kind"] == _lib.HM_KIND_FUSED and st["dom_compressions"] == 2
-    assert 1.009 <= st["dom_compressions_eff"] <= 1.011
+    assert 1.009 <= st["dom_compressions_eff"] <= 1.013
     # a scan_many batch over several chunks times every launch against one
     # origin: the union of launch intervals is positive and below the wall time
     ctx.scan_many([(b"bradfitz", 10**9 + 10**7 * i, 10**9 + 10**7 * (i + 1) - 1)
