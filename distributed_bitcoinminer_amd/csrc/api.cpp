@@ -65,7 +65,7 @@ constexpr uint32_t kQueueShiftBig = 4;
 constexpr uint64_t kBigLaunchNonces = 100000000000ull;
 // Guided tail of a fused launch (HM_OPT_FUSED_TAIL): the tasks of the last,
 // partial wave-round are cut into up to this many pieces each.
-constexpr uint32_t kFusedDefaultTail = 10;
+constexpr uint32_t kFusedDefaultTail = 2;
 
 // No C++ exception crosses the C ABI (include/hipminer.h): the entry points
 // run their bodies through guarded(), which maps an escaping exception
@@ -167,7 +167,10 @@ struct hm_ctx {
     uint32_t fused_parts = kFusedDefaultParts;  // HM_OPT_FUSED_PARTS (experiment hook)
     uint32_t fused_tail = kFusedDefaultTail;    // HM_OPT_FUSED_TAIL (1 = no split)
     bool tail_fused = true;  // HM_OPT_TAIL_FUSED: a large request's tail segments in one fused launch
-    bool host_result = true; // HM_OPT_HOST_RESULT: results stored to pinned host memory by the last fold
+    // HM_OPT_HOST_RESULT (experiment hook, off): results stored to pinned host
+    // memory by the last fold instead of a 16-B copy -- measured no faster
+    // (config 1: 0.3591 vs 0.3595 ms, profiles/r06/experiments/host_result/)
+    bool host_result = false;
     int queue_batch = 0;     // HM_OPT_QUEUE_BATCH: 0 = auto, else tasks per queue atomic (4..32)
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;

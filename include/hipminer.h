@@ -204,7 +204,7 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */
-#define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 10; ABI 1.8): the tasks
+#define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 2; ABI 1.8): the tasks
                                   of a fused launch's last, partial wave-round
                                   (tasks mod waves; the cheapest layouts, queued
                                   last) run as up to this many pieces each --
@@ -218,11 +218,11 @@ typedef struct hm_stats {
                                   launch on a low-priority stream, in the
                                   dominant launch's tail, when they fit one; 0:
                                   one launch per segment on the tail streams */
-#define HM_OPT_HOST_RESULT 16   /* experiment hook (0/1, default 1; ABI 1.8): the
-                                  call's last fold kernel stores the 16-B
+#define HM_OPT_HOST_RESULT 16   /* experiment hook (0/1, default 0; ABI 1.8): 1 =
+                                  the call's last fold kernel stores the 16-B
                                   results into pinned host memory (system-scope
-                                  stores), so no device-to-host copy follows;
-                                  0: hipMemcpyAsync readback as before 1.8    */
+                                  stores) instead of a hipMemcpyAsync readback;
+                                  measured no faster                            */
 #define HM_OPT_QUEUE_BATCH 17   /* experiment hook (0, 4, 8, 16, 32; ABI 1.8):
                                   tasks a workgroup fetches per work-queue
                                   atomic in the per-segment kernels; 0 (default)
