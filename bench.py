@@ -223,9 +223,10 @@ class QueueSampler:
     keeps each GPU's maximum: the queues and processes the GPUs actually
     carried (the line recorded only a modelled process count)."""
 
-    def __init__(self, period_s: float = 0.25):
+    def __init__(self, period_s: float = 0.25, pcis=None):
         import threading
         self.period_s, self.max, self.error, self.samples = period_s, {}, None, 0
+        self.pcis = set(pcis) if pcis else None  # report only these GPUs (PCI addresses)
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True)
 
@@ -254,10 +255,22 @@ class QueueSampler:
     def result(self) -> dict:
         if self.error and not self.samples:
             return {"error": self.error}
-        pci = kfd_gpu_pci()
-        return {"samples": self.samples, "period_s": self.period_s,
-                "max": {pci.get(g, f"gpu_id {g}"): v for g, v in sorted(self.max.items())},
-                "max_queues_any_gpu": max((v["queues"] for v in self.max.values()), default=0)}
+        per_gpu = by_pci(self.max, self.pcis)
+        return {"samples": self.samples, "period_s": self.period_s, **per_gpu,
+                "max_queues_any_gpu": max((v["queues"] for v in per_gpu["max"].values()),
+                                          default=0)}
+
+
+def by_pci(counts: dict, pcis=None) -> dict:
+    """{gpu_id: counts} keyed by PCI address instead; with `pcis`, only those
+    GPUs (the job's), the others only counted: KFD lists every process on
+    the host, other jobs' GPUs included."""
+    pci = kfd_gpu_pci()
+    named = {pci.get(g, f"gpu_id {g}"): v for g, v in sorted(counts.items())}
+    if pcis is None:
+        return {"max": named}
+    return {"max": {k: v for k, v in named.items() if k in pcis},
+            "other_gpus": sum(1 for k in named if k not in pcis)}
 
 
 def single_process_cfg4(devices, rccl: bool):
@@ -348,7 +361,8 @@ def _run_child(cmd, timeout: float) -> dict:
     return res
 
 
-def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_cmd=None) -> dict:
+def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_cmd=None,
+                       pcis=None) -> dict:
     """configs[3] through SURVEY §8(e)'s single-process model, measured by
     rank 0 after every timed region of a multi-GPU line: one hipminer context
     over every GPU in `devices`, twice, each in a FRESH CHILD PROCESS with a
@@ -359,7 +373,9 @@ def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_
     line is printed either way.  `processes_per_gpu` counts the processes
     that hold a context on each GPU while a child runs: every rank's own
     process (its torch context and communicator on its GPU, rank_gpus[r])
-    plus the child.  child_cmd(merge, devices) -> argv is a test hook."""
+    plus the child; `queues_per_gpu` per child the hardware queues KFD shows on
+    each of the job's GPUs (`pcis`, PCI addresses) while it runs.
+    child_cmd(merge, devices) -> argv is a test hook."""
     rccl_devs = sorted(set(devices))
     if child_cmd is None:
         def child_cmd(merge, devs):
@@ -379,7 +395,7 @@ def run_single_process(devices, rank_gpus, timeout: float = SP_TIMEOUT_S, child_
     for merge, devs in (("host", list(devices)), ("rccl", rccl_devs)):
         # the queues every process on each GPU holds while this child runs
         # (KFD sysfs, sampled; keyed by PCI address)
-        with QueueSampler() as qs:
+        with QueueSampler(pcis=pcis) as qs:
             res = _run_child(child_cmd(merge, devs), timeout)
         res.setdefault("devices", devs)
         res["queues_per_gpu"] = qs.result()
@@ -602,6 +618,8 @@ def roofline(st, msg, lo, hi):
     tiles_pl = -(-int(nonces_pl) // 10 ** dom_seg["V"])
     algo_bytes = tiles_pl * 128 + st["dom_grid"] * 4 * 16
     tasks_pl = int(nonces_pl) // 6400 if dom_seg["kind"] == 2 else None  # tiled unit = 64 lanes x 100
+    # tasks per queue atomic (api.cpp queue_shift): 16 for launches of >= 10^11 nonces
+    queue_batch = 16 if nonces_pl >= 1e11 else 4
     chained = dom_seg["kind"] == 3
     if chained:  # priced by what the formulation executes (see docstring)
         achieved, ops_pn, pricing = achieved_rounds, rops, "rounds"
@@ -627,10 +645,12 @@ def roofline(st, msg, lo, hi):
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": algo_bytes,
             "queue_units_per_launch": tasks_pl,
-            "queue_atomics_per_launch": -(-tasks_pl // 4) if tasks_pl is not None else None,
-            "traffic_note": "PMC traffic is the work queue's device-scope atomics "
-                            "(one per 4 dequeued tasks, executed memory-side), not "
-                            "re-reads (DESIGN.md §9)",
+            "queue_atomics_per_launch": -(-tasks_pl // queue_batch) if tasks_pl is not None
+            else None,
+            "queue_tasks_per_atomic": queue_batch,
+            "traffic_note": f"PMC traffic is the work queue's device-scope atomics "
+                            f"(one per {queue_batch} dequeued tasks, executed memory-side), "
+                            f"not re-reads (DESIGN.md §9)",
             "f_eff_ghz": f_eff,
             "frac_at_f_eff": round(achieved / (PEAK_TOPS * f_eff / 2.4), 4) if f_eff else None,
             "kernel": st["dom_kernel"],
@@ -859,11 +879,10 @@ def main():
     # regions (each rank: torch + its communicator + BENCH_STREAMS hipminer
     # streams), before any single-process child starts
     queues_after = None
+    job_pcis = sorted({d["pci_bus_id"] for d in ranks["device"]})
     if rank == 0:
         q = kfd_queues()
-        pci = kfd_gpu_pci()
-        queues_after = q if "error" in q else {pci.get(g, f"gpu_id {g}"): v
-                                               for g, v in sorted(q.items())}
+        queues_after = q if "error" in q else by_pci(q, job_pcis)
 
     # configs[3] once more through SURVEY §8(e)'s single-process model, on a
     # multi-GPU run: rank 0 starts two child processes in turn (host merge,
@@ -898,8 +917,14 @@ def main():
             if max(sp_devices) >= seen:
                 single = {"devices": sp_devices, "skipped": f"rank 0 sees {seen} GPU(s)"}
             else:
+                sp_pcis = set()
+                for d in set(sp_devices):
+                    pr = torch.cuda.get_device_properties(d)
+                    sp_pcis.add(f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:"
+                                f"{pr.pci_device_id:02x}.0")
                 single = run_single_process(sp_devices,
-                                            list(range(world)) if backend == "nccl" else [0] * world)
+                                            list(range(world)) if backend == "nccl" else [0] * world,
+                                            pcis=sp_pcis)
         if wait_group is not None:
             dist.barrier(group=wait_group)
         barrier()

@@ -251,6 +251,11 @@ def test_kfd_queue_sampler_reads_sysfs(tmp_path, monkeypatch):
     r = qs.result()
     assert r["samples"] >= 1 and r["max_queues_any_gpu"] == 3
     assert r["max"]["0000:75:00.0"] == {"queues": 3, "processes": 2}
+    with bench.QueueSampler(period_s=0.01, pcis={"0000:f5:00.0"}) as qs:
+        time.sleep(0.05)
+    r = qs.result()
+    assert r["max"] == {"0000:f5:00.0": {"queues": 1, "processes": 1}} and r["other_gpus"] == 1
+    assert r["max_queues_any_gpu"] == 1
     monkeypatch.setattr(bench, "KFD_PROC", str(tmp_path / "none"))
     with bench.QueueSampler(period_s=0.01) as qs:
         pass

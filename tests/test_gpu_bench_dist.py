@@ -88,11 +88,20 @@ def test_bench_torchrun_gloo_two_ranks_cfg2_and_cfg4():
     assert c4["nonces_rank0"] == hi - lo + 1
     sp = line["single_process"]
     assert sp["processes_per_gpu"] == {"0": 3}, sp  # both ranks and the child
+    # the queues the job's GPU carried, measured (KFD sysfs): after the timed
+    # regions, and while each child ran
+    pci = line["ranks"]["device"][0]["pci_bus_id"]
+    assert line["config"]["hip_streams_per_gpu"] == 2
+    q = line["queues_per_gpu"]
+    assert "error" in q or set(q["max"]) <= {pci}, q
     for m, merge in (("host", "none"), ("rccl", "RCCL all-gather")):
         e = sp[m]
         assert "error" not in e, e
         assert e["devices"] == [0] and e["merge"] == merge, e
         assert e["result_vs_oracle"]["match"] is True and e["mid_call_syncs"] == 0, e
+        assert e["streams_per_gpu"] == 2, e
+        qs = e["queues_per_gpu"]
+        assert "error" in qs or (qs["samples"] >= 1 and set(qs["max"]) <= {pci}), qs
 
 
 def test_bench_torchrun_rccl_world1_cfg2_and_cfg3():
