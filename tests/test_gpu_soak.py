@@ -11,6 +11,11 @@ digits over 1.3-3.2*10^7 nonces (the chained layout with a K+W table, round 3)
 under a random table cap HM_OPT_TABLE_DIGITS (1..5: 10^4..1 epochs).
 A second soak (half the budget) sends random hm_scan_many batches to fresh
 multi-"device" contexts under random stream counts and table-growth caps.
+Since round 6 each case also draws the fused launch's guided-tail pieces
+(HM_OPT_FUSED_TAIL 1/2/5/10) and the queue batch (HM_OPT_QUEUE_BATCH), and
+one case in ten is a large request (1.4-3*10^8 nonces) whose tail segments
+run as one fused launch beside the dominant kernel (HM_OPT_TAIL_FUSED on or
+off), checked against the SHA-extension oracle.
 HM_SOAK_SEED picks the sequence; a failure names its case.  HM_SOAK_FUSED=0
 sends the small requests through the per-segment kernels instead of the fused
 launch (HM_OPT_FUSED=0), which every request above 2^27 nonces takes.
@@ -33,6 +38,16 @@ def _epoch_case(rng):
     span = rng.randrange(13_000_000, 32_000_000)
     lo = 10 ** (d - 1) + rng.randrange(0, 9 * 10 ** (d - 1) - span)
     return m, lo, lo + span - 1, rng.randrange(0, 6)
+
+
+def _large_case(rng):
+    """A request above the fused size whose small digit segments form a tail
+    (round 6: one fused launch on a tail stream)."""
+    L = rng.randrange(0, 130)
+    m = bytes(rng.randrange(256) for _ in range(L))
+    c = 10 ** rng.randrange(8, 12)
+    lo = c - rng.randrange(10**6, 10**8)
+    return m, lo, lo + rng.randrange(140_000_000, 300_000_000)
 
 
 def _case(rng):
@@ -65,18 +80,32 @@ def test_random_soak_checked(ctx, oracle_mod):
     ctx.set_option(_lib.HM_OPT_FUSED, 1 if fused else 0)
     try:
         while time.time() - t0 < budget:
-            table = 0
+            table, large = 0, False
             if rng.randrange(5) == 0:
                 m, lo, hi, table = _epoch_case(rng)
+            elif rng.randrange(10) == 0:
+                m, lo, hi = _large_case(rng)
+                large = True
             else:
                 m, lo, hi = _case(rng)
-            ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, table)
+            opts = {_lib.HM_OPT_TABLE_DIGITS: table,
+                    _lib.HM_OPT_FUSED_TAIL: rng.choice([1, 2, 2, 5, 10]),
+                    _lib.HM_OPT_QUEUE_BATCH: rng.choice([0, 0, 4, 8, 16, 32]),
+                    _lib.HM_OPT_TAIL_FUSED: rng.choice([1, 1, 0]),
+                    _lib.HM_OPT_STREAMS: rng.choice([2, 2, 4, 1])}
+            for o, v in opts.items():
+                ctx.set_option(o, v)
             try:
                 got = ctx.scan_checked(m, lo, hi)
             finally:
-                ctx.set_option(_lib.HM_OPT_TABLE_DIGITS, 0)
-            exp = oracle_mod.c_scan_sum(m, lo, hi)
-            assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), (n, m.hex(), lo, hi, table)
+                for o, v in ((_lib.HM_OPT_TABLE_DIGITS, 0), (_lib.HM_OPT_FUSED_TAIL, 2),
+                             (_lib.HM_OPT_QUEUE_BATCH, 0), (_lib.HM_OPT_TAIL_FUSED, 1),
+                             (_lib.HM_OPT_STREAMS, 4)):
+                    ctx.set_option(o, v)
+            exp = oracle_mod.fast_scan_sum(m, lo, hi) if large and oracle_mod.fast_available() \
+                else oracle_mod.c_scan_sum(m, lo, hi)
+            assert (got[0], got[1], got[2]) == (tuple(exp[0]), exp[1], exp[2]), \
+                (n, m.hex(), lo, hi, sorted(opts.items()))
             n += 1
             nonces += hi - lo + 1
             if time.time() - last > 10:
@@ -108,7 +137,8 @@ def test_random_batches_fresh_contexts(oracle_mod):
     n = reqs_done = grows = 0
     while time.time() - t0 < budget:
         devs = [0] * rng.randrange(1, 4)
-        streams = rng.choice([1, 4])
+        streams = rng.choice([1, 2, 4])
+        tail_fused = rng.choice([0, 1])
         cap = rng.choice([0, 0, 10**4, 10**5])
         reqs = []
         # one batch in ten spans two hm_scan_many chunks (> kMaxBatch = 64)
@@ -122,10 +152,12 @@ def test_random_batches_fresh_contexts(oracle_mod):
         with _lib.Context(devs) as c:
             c.set_option(_lib.HM_OPT_FUSED, 0 if os.environ.get("HM_SOAK_FUSED", "1") == "0" else 1)
             c.set_option(_lib.HM_OPT_STREAMS, streams)
+            c.set_option(_lib.HM_OPT_TAIL_FUSED, tail_fused)
             c.set_option(_lib.HM_OPT_TABLE_ROWS_CAP, cap)
             got = c.scan_many(reqs)
             st = c.stats()
-        assert got == exp, (n, len(devs), streams, cap, [(m.hex(), lo, hi) for m, lo, hi in reqs])
+        assert got == exp, (n, len(devs), streams, tail_fused, cap,
+                            [(m.hex(), lo, hi) for m, lo, hi in reqs])
         assert st["mid_call_syncs"] == 0, (n, st)
         n += 1
         reqs_done += len(reqs)

@@ -26,8 +26,10 @@ NONCES = {"hm_tiled_kernel<4, false, false>": 900_000_000 + (2**32 - 10**9),
           "hm_tiled_kernel<3, false, false>": 9_990_000,
           # cfg3 (120-B message): d = 8, 9, 10 are chained
           "hm_chained_kernel": 2**32 - 10**7,
-          # cfg4's dominant segment (bradfitz d = 12): [10^11, 1.2*10^11)
-          "hm_tiled_kernel<5, true, false>": 20_000_000_000}
+          # cfg4's dominant segment (bradfitz d = 12): [10^11, 3*10^11) since
+          # round 6 (a launch of >= 10^11 nonces, which fetches 16 tasks per
+          # queue atomic, as the bench's 9*10^11-nonce launch does)
+          "hm_tiled_kernel<5, true, false>": 200_000_000_000}
 
 
 def per_dispatch(path):
