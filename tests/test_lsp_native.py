@@ -132,13 +132,16 @@ def test_idle_connection_stays_alive(tool, heartbeat, limit):
     would keep the server silent and drop it; both sides must survive many
     EpochLimits of idleness."""
     import time
-    srv = H.FakeLspServer(epoch_ms=40, epoch_limit=limit, heartbeat=heartbeat)
-    env = dict(os.environ, HM_LSP_EPOCH_MS="40", HM_LSP_EPOCH_LIMIT=str(limit))
+    # 80-ms epochs: an EpochLimit-2 drop timer of 160 ms leaves room for the
+    # scheduling jitter of a loaded host (40-ms epochs flaked under pytest -n)
+    epoch = 80
+    srv = H.FakeLspServer(epoch_ms=epoch, epoch_limit=limit, heartbeat=heartbeat)
+    env = dict(os.environ, HM_LSP_EPOCH_MS=str(epoch), HM_LSP_EPOCH_LIMIT=str(limit))
     p = subprocess.Popen([tool, "echo", srv.hostport], stdout=subprocess.PIPE, text=True, env=env)
     try:
         cid = srv.accept(timeout=30)
         assert srv.read(cid, timeout=30) == b"hello"
-        time.sleep(40 * 0.040)                          # 40 idle epochs
+        time.sleep(25 * epoch / 1000)                    # 25 idle epochs
         assert p.poll() is None and not srv.is_lost(cid)
         srv.write(cid, b"ping")
         assert srv.read(cid, timeout=30) == b"ping"
