@@ -38,6 +38,7 @@ HM_OPT_FUSED_TAIL = 14
 HM_OPT_TAIL_FUSED = 15
 HM_OPT_HOST_RESULT = 16
 HM_OPT_QUEUE_BATCH = 17
+HM_OPT_FUSED_TRACE = 18
 HM_MERGE_NONE, HM_MERGE_HOST, HM_MERGE_RCCL = 0, 1, 2
 
 
@@ -132,6 +133,9 @@ def load() -> ctypes.CDLL:
         lib.hm_scan_cpu.restype = ctypes.c_int
         lib.hm_scan_cpu.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.POINTER(hm_result)]
+        lib.hm_debug_fused_trace.restype = ctypes.c_int
+        lib.hm_debug_fused_trace.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.c_int]
         lib.hm_debug_streams_made.restype = ctypes.c_int
         lib.hm_debug_streams_made.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.hm_debug_plan.restype = ctypes.c_int
@@ -217,6 +221,15 @@ class Context:
         """HIP streams (hardware queues) the context has made on its
         device_index-th device (debug export; ABI 1.8 makes them on first use)."""
         return int(self._lib.hm_debug_streams_made(self._h, device_index))
+
+    def fused_trace(self) -> list:
+        """The last traced fused launch's timeline (HM_OPT_FUSED_TRACE):
+        per wave slot (start, last task start, end, tasks), wall-clock ticks."""
+        buf = (ctypes.c_uint64 * (4 * 32768))()
+        n = self._lib.hm_debug_fused_trace(self._h, buf, 32768)
+        if n < 0:
+            raise HipMinerError(n, "hm_debug_fused_trace")
+        return [tuple(int(x) for x in buf[4 * i: 4 * i + 4]) for i in range(n)]
 
     def set_option(self, opt: int, value: int) -> None:
         rc = self._lib.hm_set_option(self._h, opt, value)

@@ -120,6 +120,8 @@ struct Device {
     uint64_t* best = nullptr;      // [kMaxBatch][kStreams][2]: per request, per stream
     uint64_t* result = nullptr;    // [kMaxBatch][2]
     uint64_t* gathered = nullptr;  // [ndev][kMaxBatch][2] (RCCL merge)
+    uint64_t* trace = nullptr;     // HM_OPT_FUSED_TRACE: 4 x u64 per wave slot of a fused launch
+    int trace_waves = 0;           // wave slots of the last traced fused launch
     hm_result* host_out = nullptr; // pinned, fine-grained [kMaxBatch]: the 16-B readback slots
     uint64_t* host_dev = nullptr;  // host_out as the device addresses it
     hipEvent_t join[kStreams] = {};
@@ -172,6 +174,7 @@ struct hm_ctx {
     // (config 1: 0.3591 vs 0.3595 ms, profiles/r06/experiments/host_result/)
     bool host_result = false;
     int queue_batch = 0;     // HM_OPT_QUEUE_BATCH: 0 = auto, else tasks per queue atomic (4..32)
+    bool fused_trace = false; // HM_OPT_FUSED_TRACE (diagnostics): fused waves record their timeline
     // host waits on GPU work while the call is still enqueuing (hm_stats.mid_call_syncs)
     bool enqueuing = false;
     int32_t mid_syncs = 0;
@@ -279,6 +282,7 @@ void device_free(Device& dv) {
     if (dv.acc) (void)hipFree(dv.acc);
     if (dv.result) (void)hipFree(dv.result);
     if (dv.gathered) (void)hipFree(dv.gathered);
+    if (dv.trace) (void)hipFree(dv.trace);
     if (dv.host_out) (void)hipHostFree(dv.host_out);
     dv.ordinal = -1;
 }
@@ -892,6 +896,11 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     }
     fa.ntasks = (uint32_t)ids;
     fa.nbig = (uint32_t)nbig;
+    if (ctx->fused_trace) {
+        if (!dv.trace)
+            HIPCHK(hipMalloc(&dv.trace, (size_t)kMaxCandWaves * 4 * sizeof(uint64_t)));
+        fa.trace = dv.trace;
+    }
     fa.nparts = nparts > 1 ? nparts : 1;
     fa.nseg = pa.nseg = (uint32_t)segs.size();
     pa.njobs = (uint32_t)jobs;
@@ -905,6 +914,7 @@ int enqueue_fused(hm_ctx* ctx, Device& dv, const MsgPlan& mp, std::vector<SegPla
     // with static first tasks the queue starts past every wave slot
     pa.counter0 = (fa.flags & kFusedStaticFirst) ? (uint32_t)grid * (kBlock / kWaveSize) : 0;
     HIPCHK(launch_fused_plan(pa, st));
+    if (fa.trace) dv.trace_waves = grid * (kBlock / kWaveSize);
     Launch L;
     rc = next_event(dv, &L.start);
     if (rc) return rc;
@@ -1372,6 +1382,9 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
             if (value != 1 && value != 2 && value != 5 && value != 10) return HM_ERR_INVALID;
             ctx->fused_parts = (uint32_t)value;
             return HM_OK;
+        case HM_OPT_FUSED_TRACE:
+            ctx->fused_trace = value != 0;
+            return HM_OK;
         case HM_OPT_QUEUE_BATCH:
             if (value != 0 && value != 4 && value != 8 && value != 16 && value != 32)
                 return HM_ERR_INVALID;
@@ -1597,6 +1610,22 @@ int hm_scan_stats_sized(const hm_ctx* ctx, hm_stats* out, size_t size) {
 size_t hm_debug_code_object(const unsigned char** p) {
     if (p) *p = hm_scan_code_object;
     return (size_t)(hm_scan_code_object_end - hm_scan_code_object);
+}
+
+// The timeline of the last traced fused launch on device 0 (HM_OPT_FUSED_TRACE):
+// up to `cap` wave slots x 4 u64 -- wall_clock64 at the wave's start, at its
+// last task's start, at its end, and its task count.  Returns the launch's
+// wave slots (0: none traced).  Diagnostics (tools/fused_trace.py).
+int hm_debug_fused_trace(hm_ctx* ctx, uint64_t* out, int cap) {
+    if (!ctx || !out || cap < 0) return HM_ERR_INVALID;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    if (ctx->abandoned) return HM_ERR_TIMEOUT;
+    Device& dv = ctx->devs[0];
+    if (!dv.trace || !dv.trace_waves) return 0;
+    HIPCHK(hipSetDevice(dv.ordinal));
+    const int n = std::min(cap, dv.trace_waves);
+    int rc = host_read(ctx, out, dv.trace, (size_t)n * 4 * sizeof(uint64_t));
+    return rc ? rc : dv.trace_waves;
 }
 
 // Streams (hardware queues) made so far on device i of ctx (make_streams):

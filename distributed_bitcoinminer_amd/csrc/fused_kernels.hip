@@ -163,11 +163,19 @@ DEV void fused_body(FusedArgsK* A) {
         if (__lane_id() == 0) t = atomicAdd(A->counter, 1u);
         return t;
     };
+    uint64_t* const trace = A->trace;  // diagnostics, normally null
+    uint64_t t_start = 0, t_last = 0;
+    uint32_t ntask = 0;
+    if (trace) t_start = wall_clock64();
     uint32_t next = (flags & (kFusedStaticFirst | kFusedStatic)) ? wslot : dequeue();
     const uint32_t nbig = A->nbig, nparts = A->nparts;
     for (;;) {
         const uint32_t id = uni(next);
         if (id >= A->ntasks) break;
+        if (trace) {
+            t_last = wall_clock64();
+            ++ntask;
+        }
         next = 0;
         if (flags & kFusedStatic) next = id + nwaves;
         else if (flags & kFusedPrefetch) next = dequeue();
@@ -206,6 +214,12 @@ DEV void fused_body(FusedArgsK* A) {
         if (!(flags & (kFusedPrefetch | kFusedStatic))) next = dequeue();
     }
     wave_store<CSUM>(A->cand, A->sums, wslot, best, sums);
+    if (trace && __lane_id() == 0) {
+        trace[4 * (size_t)wslot] = t_start;
+        trace[4 * (size_t)wslot + 1] = t_last;
+        trace[4 * (size_t)wslot + 2] = wall_clock64();
+        trace[4 * (size_t)wslot + 3] = ntask;
+    }
 }
 
 #undef HM_FUSED_CASE_S

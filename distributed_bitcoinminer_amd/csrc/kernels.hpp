@@ -174,6 +174,10 @@ struct FusedArgs {
     uint32_t r;           // prefix-remainder bytes (generic)
     uint32_t pw[16];      // prefix remainder words (generic)
     uint32_t mid[8];      // midstate (generic)
+    // diagnostics (HM_OPT_FUSED_TRACE): per wave slot w, [4w..4w+3] = the
+    // constant-rate wall clock (wall_clock64) at the wave's start, when it
+    // takes its last task, at its end, and the tasks it ran; null = off
+    uint64_t* trace;
     FusedSeg segs[kMaxFusedSegs];
 };
 

@@ -227,6 +227,9 @@ typedef struct hm_stats {
                                   tasks a workgroup fetches per work-queue
                                   atomic in the per-segment kernels; 0 (default)
                                   = 4, and 16 for launches of >= 10^11 nonces */
+#define HM_OPT_FUSED_TRACE 18   /* diagnostics (0/1; ABI 1.8): fused launches on
+                                  device 0 record each wave's timeline
+                                  (tools/fused_trace.py)                        */
 #define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
                                   a call blocks until its GPU work is done; > 0 =
                                   a call returns HM_ERR_TIMEOUT (and abandons the

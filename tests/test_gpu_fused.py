@@ -258,3 +258,21 @@ def test_results_stored_to_host_or_copied_agree(oracle_mod):
                 assert c.scan_many(reqs) == exp, (devs, rccl, host)
                 for (m, a, b), e in zip(reqs, exp):
                     assert c.scan(m, a, b) == e, (devs, rccl, host, m, a, b)
+
+
+def test_fused_trace_diagnostics(oracle_mod):
+    """HM_OPT_FUSED_TRACE (diagnostics, tools/fused_trace.py): every wave of the
+    fused launch records its start, last-task and end times and its task
+    count; the answers do not change and the waves' tasks cover the launch."""
+    with _lib.Context([0]) as c:
+        assert c.fused_trace() == []  # nothing traced yet
+        c.set_option(_lib.HM_OPT_FUSED_TRACE, 1)
+        assert c.scan(b"bradfitz", 0, 10**7 + 1) == (356393768206, 7645578)
+        tr = c.fused_trace()
+        st = c.stats()
+        assert len(tr) == st["dom_grid"] * 4, (len(tr), st)
+        assert all(t[0] <= t[1] <= t[2] for t in tr if t[3] > 0)
+        # 10^7 + 2 nonces: >= 15,625 tiled tasks of 640 nonces, plus pieces
+        assert sum(t[3] for t in tr) >= 15_625
+        m = b"z" * 120
+        assert c.scan(m, 0, 10**6) == oracle_mod.c_scan(m, 0, 10**6)
