@@ -1375,7 +1375,7 @@ int hm_set_option(hm_ctx* ctx, int opt, int64_t value) {
             ctx->fused = value != 0;
             return HM_OK;
         case HM_OPT_FUSED_FLAGS:
-            if (value < 0 || value > 15) return HM_ERR_INVALID;
+            if (value < 0 || value > 31) return HM_ERR_INVALID;
             ctx->fused_flags = (uint32_t)value;
             return HM_OK;
         case HM_OPT_FUSED_PARTS:

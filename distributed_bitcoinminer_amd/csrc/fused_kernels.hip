@@ -172,10 +172,15 @@ DEV void fused_body(FusedArgsK* A) {
     for (;;) {
         const uint32_t id = uni(next);
         if (id >= A->ntasks) break;
-        if (trace) {
-            t_last = wall_clock64();
-            ++ntask;
+        if (trace) t_last = wall_clock64();
+        if (flags & kFusedPrioEq) {
+            // s_setprio takes an immediate
+            if (ntask == 0) __builtin_amdgcn_s_setprio(3);
+            else if (ntask == 1) __builtin_amdgcn_s_setprio(2);
+            else if (ntask == 2) __builtin_amdgcn_s_setprio(1);
+            else if (ntask == 3) __builtin_amdgcn_s_setprio(0);
         }
+        ++ntask;
         next = 0;
         if (flags & kFusedStatic) next = id + nwaves;
         else if (flags & kFusedPrefetch) next = dequeue();

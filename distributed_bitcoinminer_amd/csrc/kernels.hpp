@@ -155,6 +155,12 @@ constexpr uint32_t kFusedStaticFirst = 1;  // first task = the wave's slot; the 
 constexpr uint32_t kFusedPrefetch = 2;     // dequeue the next task id while running the current one
 constexpr uint32_t kFusedStatic = 4;       // no queue: wave w runs tasks w, w + nwaves, w + 2 nwaves, ...
 constexpr uint32_t kFusedLds = 8;          // dequeue through the workgroup's LDS dispenser (scan_tasks.hpp)
+// the SIMD's arbiter issues from the oldest wave first, so the youngest waves
+// of a SIMD hold their first task for most of a small launch and finish it
+// alone at the end (tools/fused_trace.py): with kFusedPrioEq a wave's
+// priority (s_setprio) falls with the tasks it has run, 3, 2, 1, 0, so the
+// waves of a SIMD progress together
+constexpr uint32_t kFusedPrioEq = 16;
 
 // Guided tail of the fused launch (round 6): task ids below `nbig` run one
 // whole task each; the tasks of the last, partial wave-round (the cheapest

@@ -193,14 +193,15 @@ typedef struct hm_stats {
                                   fused launch runs as ONE planner + ONE scan
                                   launch (HM_KIND_FUSED); 0: one launch per
                                   digit segment (ABI 1.7)                       */
-#define HM_OPT_FUSED_FLAGS 11   /* experiment hook (0..15): how the fused launch's
+#define HM_OPT_FUSED_FLAGS 11   /* experiment hook (0..31): how the fused launch's
                                   waves get tasks -- bit 0: first task = the
                                   wave's slot (no opening burst of queue
                                   atomics); bit 1: dequeue the next task while
                                   the current one runs; bit 2: no queue, wave
                                   slots strided over the task ids; bit 3:
                                   dequeue through the workgroup's LDS
-                                  dispenser (ABI 1.7)                           */
+                                  dispenser (ABI 1.7); bit 4: a wave's priority
+                                  falls with the tasks it ran (ABI 1.8)         */
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */

@@ -156,7 +156,7 @@ def test_fused_parts_option_validated(ctx):
             ctx.set_option(_lib.HM_OPT_FUSED_PARTS, bad)
 
 
-@pytest.mark.parametrize("flags", [0, 2, 3, 4, 8, 9])
+@pytest.mark.parametrize("flags", [0, 2, 3, 4, 8, 9, 17, 25])
 def test_task_dispensing_flags_checked(ctx, oracle_mod, flags):
     """HM_OPT_FUSED_FLAGS: every way the fused launch's waves get their tasks
     (queue, static first task, prefetch, static stride, LDS dispenser) hashes
