@@ -133,6 +133,9 @@ def load() -> ctypes.CDLL:
         lib.hm_scan_cpu.restype = ctypes.c_int
         lib.hm_scan_cpu.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
                                     ctypes.c_int, ctypes.POINTER(hm_result)]
+        lib.hm_debug_auto_deadline_ms.restype = ctypes.c_double
+        lib.hm_debug_auto_deadline_ms.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_int]
         lib.hm_debug_fused_trace.restype = ctypes.c_int
         lib.hm_debug_fused_trace.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                              ctypes.c_int]

@@ -1423,21 +1423,26 @@ namespace {
 constexpr double kDeadlineFloorMs = 2000.0;
 constexpr double kDeadlineSlack = 8.0;
 
-double auto_deadline_ms(const hm_ctx* ctx, const hm_request* reqs, int n) {
+double modelled_deadline_ms(const hm_request* reqs, int n, bool force_generic, int table_digits,
+                            double simds) {
     static const uint8_t empty_msg = 0;
     long double cycles = 0;
     for (int r = 0; r < n; ++r) {
         const hm_request& q = reqs[r];
         if (q.lo > q.hi) continue;
         const MsgPlan mp = plan_message(q.msg ? q.msg : &empty_msg, q.msg ? q.len : 0);
-        for (const SegPlan& g : plan_range(mp, q.lo, q.hi, ctx->force_generic, ctx->table_digits))
+        for (const SegPlan& g : plan_range(mp, q.lo, q.hi, force_generic, table_digits))
             cycles += ((long double)(g.hi - g.lo) + 1) * seg_cost(g) / kWaveSize;
     }
+    return kDeadlineFloorMs + kDeadlineSlack * (double)(cycles / (long double)simds / 2.4e6L);
+}
+
+double auto_deadline_ms(const hm_ctx* ctx, const hm_request* reqs, int n) {
     std::vector<int> ords;
     for (const auto& dv : ctx->devs)
         if (std::find(ords.begin(), ords.end(), dv.ordinal) == ords.end()) ords.push_back(dv.ordinal);
-    const long double simds = 4.0L * ctx->devs[0].cus * (long double)ords.size();
-    return kDeadlineFloorMs + kDeadlineSlack * (double)(cycles / simds / 2.4e6L);
+    return modelled_deadline_ms(reqs, n, ctx->force_generic, ctx->table_digits,
+                                4.0 * ctx->devs[0].cus * (double)ords.size());
 }
 
 // hm_scan_many with ctx->mu held.
@@ -1626,6 +1631,18 @@ int hm_debug_fused_trace(hm_ctx* ctx, uint64_t* out, int cap) {
     const int n = std::min(cap, dv.trace_waves);
     int rc = host_read(ctx, out, dv.trace, (size_t)n * 4 * sizeof(uint64_t));
     return rc ? rc : dv.trace_waves;
+}
+
+// HM_OPT_DEADLINE_MS = -1's deadline for one request on `cus` compute units
+// (host-only; tests/test_abi.py checks the model without a GPU).
+double hm_debug_auto_deadline_ms(const uint8_t* msg, size_t len, uint64_t lo, uint64_t hi,
+                                 int cus) {
+    const hm_request q{msg, msg ? len : 0, lo, hi};
+    try {
+        return modelled_deadline_ms(&q, 1, false, 0, 4.0 * cus);
+    } catch (...) {
+        return -1.0;
+    }
 }
 
 // Streams (hardware queues) made so far on device i of ctx (make_streams):

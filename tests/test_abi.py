@@ -213,3 +213,25 @@ def test_host_blocking_calls_only_in_counting_helpers():
             if blocking.search(line) and current not in allowed:
                 stray.append(f"{name}:{no} in {current}: {line.strip()}")
     assert not stray, stray
+
+
+def test_auto_deadline_model():
+    """HM_OPT_DEADLINE_MS = -1 (ABI 1.8): 2 s + 8 x the modelled kernel time
+    (seg_cost: measured SIMD cycles per 64 nonces per layout, over 4 SIMDs per
+    CU at 2.4 GHz).  Host-only: the model a GPU miner's deadline comes from."""
+    lib = _lib.load()
+
+    def dl(msg, lo, hi, cus=256):
+        return lib.hm_debug_auto_deadline_ms(msg, len(msg), lo, hi, cus)
+    assert dl(b"bradfitz", 5, 4) == 2000.0                    # empty range
+    assert 2000 < dl(b"bradfitz", 0, 10**7 + 1) < 2010        # config 1: ~0.3 ms of kernels
+    cfg2 = dl(b"bradfitz", 0, 2**32 - 1)
+    # 2^32 nonces at ~4150 SIMD cycles / 64 nonces on 1024 SIMDs: ~0.11 s
+    assert 2800 < cfg2 < 3000, cfg2
+    cfg4 = dl(b"bradfitz", 0, 2**40 - 1)
+    assert 200_000 < cfg4 < 260_000, cfg4                    # ~29 s of kernels, x 8
+    assert dl(b"bradfitz", 0, 2**32 - 1, cus=128) > cfg2      # fewer CUs: later deadline
+    # the 120-B message runs C = 2 layouts partly: a later deadline than cfg2's
+    import bench
+    assert dl(bench.long120(), 0, 2**32 - 1) > 2000
+    assert dl(b"", (1 << 64) - 10, (1 << 64) - 1) < 2001
