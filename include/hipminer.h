@@ -205,6 +205,18 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_PARTS 12   /* experiment hook (1, 2, 5, 10; default 1): a
                                   tiled task of the fused launch covers 10 /
                                   parts steps of its units loop (ABI 1.7)       */
+#define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
+                                  a call blocks until its GPU work is done; > 0 =
+                                  a call returns HM_ERR_TIMEOUT (and abandons the
+                                  context) once this many ms have passed since it
+                                  began; -1 = auto: 2 s + 8 x the call's modelled
+                                  kernel time (the layouts' measured cost, the
+                                  model hm_partition balances with).  The host
+                                  then polls the GPU instead of blocking on it.
+                                  A miner whose LSP thread keeps heartbeating
+                                  would otherwise hold its chunk forever: the
+                                  server reassigns only dropped miners
+                                  (server.go:326-376)                           */
 #define HM_OPT_FUSED_TAIL 14    /* 1, 2, 5 or 10 (default 2; ABI 1.8): the tasks
                                   of a fused launch's last, partial wave-round
                                   (tasks mod waves; the cheapest layouts, queued
@@ -231,18 +243,6 @@ typedef struct hm_stats {
 #define HM_OPT_FUSED_TRACE 18   /* diagnostics (0/1; ABI 1.8): fused launches on
                                   device 0 record each wave's timeline
                                   (tools/fused_trace.py)                        */
-#define HM_OPT_DEADLINE_MS 13   /* ABI 1.8 (SURVEY §8(b) liveness): 0 (default) =
-                                  a call blocks until its GPU work is done; > 0 =
-                                  a call returns HM_ERR_TIMEOUT (and abandons the
-                                  context) once this many ms have passed since it
-                                  began; -1 = auto: 2 s + 8 x the call's modelled
-                                  kernel time (the layouts' measured cost, the
-                                  model hm_partition balances with).  The host
-                                  then polls the GPU instead of blocking on it.
-                                  A miner whose LSP thread keeps heartbeating
-                                  would otherwise hold its chunk forever: the
-                                  server reassigns only dropped miners
-                                  (server.go:326-376)                           */
 
 /* bitcoin.Hash (hash.go:13-17) evaluated on the host.  Not the hot path: used
  * to verify single results and for planning; needs no GPU. */
