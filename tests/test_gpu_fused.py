@@ -245,10 +245,19 @@ def test_results_stored_to_host_or_copied_agree(oracle_mod):
     """HM_OPT_HOST_RESULT (round 6 experiment hook, default off): the call's
     last fold kernel stores the 16-B results in pinned host memory instead of
     the copy back.  Same answers on one device, a batch, a two-device host
-    merge and the RCCL merge."""
+    merge and the RCCL merge, fused requests and a tail-fused one included."""
+    # the last request has tail segments (d <= 8) that run as one fused
+    # launch on a tail stream beside its dominant d = 9 launch
     reqs = [(b"bradfitz", 0, 10**7 + 1), (b"thom yorke", 10**9, 10**9 + 2 * 10**8),
-            (b"x" * 120, 0, 99_999), (b"", 5, 4)]
-    exp = [oracle_mod.c_scan(m, a, b) if a <= b else (MAX, 0) for m, a, b in reqs]
+            (b"x" * 120, 0, 99_999), (b"", 5, 4), (b"jonny greenwood", 0, 2 * 10**8)]
+
+    def oracle(m, a, b):
+        if a > b:
+            return (MAX, 0)
+        if b - a > 10**7 and oracle_mod.fast_available():
+            return tuple(oracle_mod.fast_scan_sum(m, a, b)[0])
+        return oracle_mod.c_scan(m, a, b)
+    exp = [oracle(m, a, b) for m, a, b in reqs]
     for devs, rccl in (([0], False), ([0, 0], False), ([0], True)):
         with _lib.Context(devs) as c:
             if rccl:
