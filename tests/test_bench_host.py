@@ -90,6 +90,13 @@ def test_roofline_prices_the_tiled_kernel_at_1552_per_compression(monkeypatch):
     assert rl["frac"] == rl["frac_algorithmic_C"]
     assert rl["frac_rounds"] < rl["frac"]
     assert rl["queue_units_per_launch"] == 4_194_967_296 // 2 // 6400
+    assert rl["queue_tasks_per_atomic"] == 4
+    # a launch of >= 10^11 nonces (cfg4's d = 12) fetches 16 tasks per atomic
+    st4 = dict(st, dom_launches=1, dom_kernel_ms=23900.0, dom_nonces=900_000_000_000,
+               dom_kernel="hm_tiled_kernel<5, true, false>")
+    rl4 = bench.roofline(st4, b"bradfitz", 0, 2**40 - 1)
+    assert rl4["queue_tasks_per_atomic"] == 16
+    assert rl4["queue_atomics_per_launch"] == -(-(900_000_000_000 // 6400) // 16)
 
 
 def test_rounds_ops_of_the_tiled_kernel():
