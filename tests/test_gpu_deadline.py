@@ -175,3 +175,22 @@ def test_miner_with_an_invisible_ordinal_falls_back(oracle_mod):
     err = p.stderr.read()
     assert p.returncode == 0, err
     assert "NO GPU" in err and "invalid argument" in err, err
+
+
+def test_deadline_on_a_two_device_context_and_checked_scans(oracle_mod):
+    """The deadline covers every device of a context (Context([0, 0]): two
+    shards, both polled) and hm_scan_checked; a generous deadline changes no
+    answer, a 1-ms one abandons the context, whose close does not wait."""
+    with _lib.Context([0, 0]) as c:
+        c.set_option(_lib.HM_OPT_DEADLINE_MS, 60_000)
+        m = b"thom yorke"
+        assert c.scan_checked(m, 10**9 - 10**6, 10**9 + 10**6) == \
+            oracle_mod.c_scan_sum(m, 10**9 - 10**6, 10**9 + 10**6)
+        assert c.scan(b"bradfitz", 0, 2**32 - 1) == (5256245051, 1626825724)
+        assert c.stats()["deadline_ms"] == 60_000
+        c.set_option(_lib.HM_OPT_DEADLINE_MS, 1)
+        with pytest.raises(_lib.HipMinerError) as ei:
+            c.scan_checked(b"bradfitz", LO, HI)
+        assert ei.value.rc == _lib.HM_ERR_TIMEOUT
+        t = time.perf_counter()
+    assert time.perf_counter() - t < 0.05  # hm_close of the abandoned context
